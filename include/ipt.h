@@ -1,0 +1,127 @@
+/*
+ * ipt.h -- C ABI of the MI355X-native inverse path tracer
+ * (inverse_path_tracer_amd/lib/libipt_amd.so, also installed as
+ * build/libpt.so and build/libipt.so so the reference's ipt_cuda.py loads it
+ * unchanged).
+ *
+ * Part 1 is the reference's own FFI surface, symbol for symbol, with the
+ * reference's signatures (the reference's ctypes caller sets no argtypes, so
+ * these are plain C ints and pointers).  Part 2 is the explicit-parameter API
+ * the reference hard-codes at compile time (scene.h:3-13), plus the adjoint.
+ *
+ * Errors: the reference exit(1)s on bad input and ignores CUDA errors.  Here
+ * no entry point exits; failures return -1 (or leave outputs untouched for the
+ * void legacy symbols) and ipt_last_error() says why (thread-local).
+ */
+#ifndef IPT_H
+#define IPT_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ */
+/* Part 1: reference symbols                                           */
+/* ------------------------------------------------------------------ */
+
+/* Replaces scene.h:177-193 loadScene.  Builds the scene from n object
+ * records (pos/ori/scl float[3] each, OBJ path, MTL path or inline
+ * "*Kd r g b*") and uploads it to the current HIP device.  Returns the
+ * triangle count nT (the reference's return value) or -1 on error, in which
+ * case *scenePtr = NULL. */
+int loadScene(float **poss, float **oris, float **scls, char **obj_fs, char **mtl_fs, int n,
+              void **scenePtr);
+
+/* Replaces scene.h:195-199 freeScene. */
+void freeScene(void *scenePtr);
+
+/* Replaces path_trace.cu:227-234 createImage: renders the legacy
+ * configuration (500x500, 100 spp, unbounded bounces, seed = time(NULL)
+ * unless ipt_legacy_config() set one) and writes an RGB8 PNG tonemapped
+ * with 255*x/(1+x). */
+void createImage(void *scenePtr, char *img_file);
+
+/* Replaces inv_path_trace.cu:195-208 createGraph: renders the transport
+ * graph against the target PNG (must match the legacy image size) and
+ * writes (nT+1)*nT*7 floats: weights[(nT+1)*nT] | pixel[(nT+1)*nT*3] |
+ * light[(nT+1)*nT*3] (ipt_cuda.py:145-163 layout; eye row last). */
+void createGraph(void *scenePtr, char *imgFile, float *data);
+
+/* Replace inv_path_trace.cu:210-221: per-triangle diffuse Kd, nT*3 floats,
+ * object-major then triangle, RGB inner (scene.h:145-162). */
+void getMaterials(void *scenePtr, float *materials);
+void setMaterials(void *scenePtr, float *materials);
+
+/* ------------------------------------------------------------------ */
+/* Part 2: explicit API                                                */
+/* ------------------------------------------------------------------ */
+
+/* Render configuration.  max_bounces < 0 reproduces the reference
+ * (paths end only by Russian roulette or a miss); max_bounces = B allows B
+ * continuation rays and does next-event estimation at the (B+1)-th vertex.
+ * Sample s of pixel (r,c) has global index (r*width + c)*spp + s and RNG
+ * seed `seed + index` (curand_init(seed+index, 0, 0)).  Only rows
+ * [row_begin, row_end) are traced (sharding); images cover those rows. */
+typedef struct ipt_params {
+  int32_t width, height, spp, max_bounces;
+  uint64_t seed;
+  int32_t row_begin, row_end;
+} ipt_params_t;
+
+const char *ipt_last_error(void);
+void ipt_clear_error(void);
+int ipt_abi_version(void);            /* 1 */
+int ipt_device_count(void);
+
+/* Legacy-symbol configuration (defaults 500, 500, 100, -1, seed -1 = time). */
+void ipt_legacy_config(int width, int height, int spp, int max_bounces, int64_t seed);
+
+/* Same as loadScene with flat arrays (pos/ori/scl: n*3 floats). */
+int ipt_load_scene(int n, const float *pos, const float *ori, const float *scl, const char **obj_files,
+                   const char **mtl_files, void **scenePtr);
+/* Host-only scene (no device buffers): export / materials only; render
+ * entry points fail on it.  Lets CPU-only tooling check scene ingest. */
+int ipt_load_scene_host(int n, const float *pos, const float *ori, const float *scl, const char **obj_files,
+                        const char **mtl_files, void **scenePtr);
+int ipt_scene_num_triangles(void *scene);
+int ipt_scene_num_emissives(void *scene);
+/* nT*57 floats: v0..v2, vertex normals, face normal, centre, area, Kd, Ks,
+ * Ke, shininess, three edge planes, sampling frame, emissive index. */
+int ipt_scene_export_triangles(void *scene, float *out);
+/* getMaterials / setMaterials with a status (nT*3 floats, host memory). */
+int ipt_scene_get_materials(void *scene, float *kd);
+int ipt_scene_set_materials(void *scene, const float *kd);
+int ipt_scene_camera(void *scene, float *out16);
+
+/* Host-memory entry points (synchronous). */
+int ipt_render_samples_host(void *scene, const ipt_params_t *p, float *samples); /* rows*W*spp*3 */
+int ipt_render_host(void *scene, const ipt_params_t *p, float *hdr, uint8_t *ldr); /* rows*W*3 */
+int ipt_adjoint_host(void *scene, const ipt_params_t *p, const float *adj /*H*W*3*/, double *grad /*nT*3*/);
+int ipt_graph_host(void *scene, const ipt_params_t *p, const uint8_t *target /*H*W*3*/,
+                   double *acc /*nullable, (nT+1)*nT*8*/, float *data /*nullable, (nT+1)*nT*7*/);
+/* DataWrapper::compress (inv_scene.h:87-115) of fp64 accumulators. */
+int ipt_compress(int nT, const double *acc, float *data);
+
+/* Device-memory entry points: pointers are device pointers, `stream` a
+ * hipStream_t (NULL = null stream); asynchronous.  kd_dev (nT*3) overrides
+ * the scene's materials when non-NULL.  grad_dev / acc_dev ACCUMULATE (zero
+ * them first). */
+int ipt_render_dev(void *scene, const ipt_params_t *p, const float *kd_dev, float *hdr_dev, uint8_t *ldr_dev,
+                   void *stream);
+int ipt_render_samples_dev(void *scene, const ipt_params_t *p, const float *kd_dev, float *samples_dev,
+                           void *stream);
+int ipt_pixel_mean_dev(const float *samples_dev, int64_t npix, int spp, float *hdr_dev, uint8_t *ldr_dev,
+                       void *stream);
+int ipt_adjoint_dev(void *scene, const ipt_params_t *p, const float *kd_dev, const float *adj_dev, double *grad_dev,
+                    void *stream);
+int ipt_graph_dev(void *scene, const ipt_params_t *p, const uint8_t *target_dev, double *acc_dev, void *stream);
+
+/* PNG helpers (RGB8). ipt_png_read with rgb == NULL only reports the size. */
+int ipt_png_write(const char *path, int width, int height, const uint8_t *rgb);
+int ipt_png_read(const char *path, int *width, int *height, uint8_t *rgb, int64_t capacity);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

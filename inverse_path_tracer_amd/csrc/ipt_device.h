@@ -1,0 +1,274 @@
+// ipt_device.h -- device-side building blocks of the MI355X path tracer.
+//
+// Everything here follows the canonical arithmetic of DESIGN.md §3 (the same
+// arithmetic the CPU oracle states), so kernel results are bit-identical to
+// the oracle on equal seeds:
+//   * fp32 dot products as fmaf chains (the contraction nvcc --fmad=true
+//     applies to the reference's Eigen (x+y)+z reductions), IEEE division and
+//     sqrt (hipcc's default correctly-rounded lowering), -ffp-contract=off so
+//     no other contraction happens;
+//   * the reference's double-precision pow(r,0.5) == sqrt, its sin/cos(phi)
+//     as a double Taylor evaluation rounded once to float;
+//   * cuRAND XORWOW seeded exactly like curand_init(seed + sample, 0, 0).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "scene_layout.h"
+
+namespace ipt {
+namespace dev {
+
+// ------------------------------------------------------------ constants
+// scene_basics.h:13-14 compare a float against the double literals 1e-4 and
+// 1e-2.  For a float x, (double)x < 1e-4  <=>  x < kMinDotUp, where kMinDotUp
+// is the smallest float above 1e-4 (1e-4 itself is not a float); same for
+// EPSILON.  tests/test_constants.py re-derives both.
+constexpr float kMinDotUp = 0x1.a36e30p-14f;   // nextafterf(1e-4 rounded down, +inf)
+constexpr float kEpsUp = 0x1.47ae16p-7f;       // smallest float > 1e-2
+constexpr float kPRR = 0.9f;                   // scene.h:11
+constexpr float kPiF = 3.14159265358979323846f;        // (float)M_PI
+constexpr float kInvPiF = (float)(1.0 / 3.14159265358979323846);  // (float)(1/M_PI)
+constexpr double kPi = 3.14159265358979323846;
+
+// ------------------------------------------------------------ XORWOW
+struct Rng {
+  uint32_t d, v0, v1, v2, v3, v4;
+};
+__device__ __forceinline__ void rng_init(Rng &s, uint64_t seed) {
+  uint32_t s0 = ((uint32_t)seed) ^ 0xaad26b49u;
+  uint32_t s1 = ((uint32_t)(seed >> 32)) ^ 0xf7dcefddu;
+  uint32_t t0 = 1099087573u * s0;
+  uint32_t t1 = 2591861531u * s1;
+  s.d = 6615241u + t1 + t0;
+  s.v0 = 123456789u + t0;
+  s.v1 = 362436069u ^ t0;
+  s.v2 = 521288629u + t1;
+  s.v3 = 88675123u ^ t1;
+  s.v4 = 5783321u + t0;
+}
+__device__ __forceinline__ float uniform(Rng &s) {
+  uint32_t t = s.v0 ^ (s.v0 >> 2);
+  s.v0 = s.v1;
+  s.v1 = s.v2;
+  s.v2 = s.v3;
+  s.v3 = s.v4;
+  s.v4 = (s.v4 ^ (s.v4 << 4)) ^ (t ^ (t << 1));
+  s.d += 362437u;
+  return (float)(s.v4 + s.d) * 2.3283064e-10f + 1.1641532e-10f;
+}
+
+// ------------------------------------------------------------ f64 helpers
+__device__ __forceinline__ void sincos_f(float xf, float &sf, float &cf) {
+  const double x = (double)xf;
+  const double k = rint(x * 0.6366197723675814);
+  double r = fma(-k, 1.5707963267948966, x);
+  r = fma(-k, 6.123233995736766e-17, r);
+  const double z = r * r;
+  double ps = 2.8114572543455206e-15;
+  ps = fma(ps, z, -7.647163731819816e-13);
+  ps = fma(ps, z, 1.6059043836821613e-10);
+  ps = fma(ps, z, -2.505210838544172e-08);
+  ps = fma(ps, z, 2.7557319223985893e-06);
+  ps = fma(ps, z, -0.0001984126984126984);
+  ps = fma(ps, z, 0.008333333333333333);
+  ps = fma(ps, z, -0.16666666666666666);
+  const double s = fma(ps * z, r, r);
+  double pc = -1.5619206968586225e-16;
+  pc = fma(pc, z, 4.779477332387385e-14);
+  pc = fma(pc, z, -1.1470745597729725e-11);
+  pc = fma(pc, z, 2.08767569878681e-09);
+  pc = fma(pc, z, -2.755731922398589e-07);
+  pc = fma(pc, z, 2.48015873015873e-05);
+  pc = fma(pc, z, -0.001388888888888889);
+  pc = fma(pc, z, 0.041666666666666664);
+  pc = fma(pc, z, -0.5);
+  const double c = fma(pc, z, 1.0);
+  const int q = ((int)k) & 3;
+  const double so = (q == 0) ? s : (q == 1) ? c : (q == 2) ? -s : -c;
+  const double co = (q == 0) ? c : (q == 1) ? -s : (q == 2) ? -c : s;
+  sf = (float)so;
+  cf = (float)co;
+}
+
+__device__ inline double log_d(double x) {
+  if (!(x > 0.0)) return x == 0.0 ? -__builtin_inf() : __builtin_nan("");
+  if (x == __builtin_inf()) return x;
+  uint64_t b = (uint64_t)__double_as_longlong(x);
+  int e = (int)((b >> 52) & 0x7ff);
+  if (e == 0) {
+    x = x * 18014398509481984.0;
+    b = (uint64_t)__double_as_longlong(x);
+    e = (int)((b >> 52) & 0x7ff) - 54;
+  }
+  e -= 1023;
+  double m = __longlong_as_double((long long)((b & 0x000fffffffffffffull) | 0x3ff0000000000000ull));
+  if (m > 1.4142135623730951) {
+    m *= 0.5;
+    e += 1;
+  }
+  const double s = (m - 1.0) / (m + 1.0);
+  const double z = s * s;
+  double p = 1.0 / 23.0;
+  p = fma(p, z, 1.0 / 21.0);
+  p = fma(p, z, 1.0 / 19.0);
+  p = fma(p, z, 1.0 / 17.0);
+  p = fma(p, z, 1.0 / 15.0);
+  p = fma(p, z, 1.0 / 13.0);
+  p = fma(p, z, 1.0 / 11.0);
+  p = fma(p, z, 1.0 / 9.0);
+  p = fma(p, z, 1.0 / 7.0);
+  p = fma(p, z, 1.0 / 5.0);
+  p = fma(p, z, 1.0 / 3.0);
+  const double lm = 2.0 * fma(p * z, s, s);
+  const double de = (double)e;
+  return fma(de, 0.6931471805599453, fma(de, 2.3190468138462996e-17, lm));
+}
+__device__ inline double exp_d(double x) {
+  if (x != x) return x;
+  if (x > 709.0) return __builtin_inf();
+  if (x < -745.0) return 0.0;
+  const double k = rint(x * 1.4426950408889634);
+  double r = fma(-k, 0.6931471805599453, x);
+  r = fma(-k, 2.3190468138462996e-17, r);
+  double p = 1.0 / 355687428096000.0;
+  p = fma(p, r, 1.0 / 20922789888000.0);
+  p = fma(p, r, 1.0 / 1307674368000.0);
+  p = fma(p, r, 1.0 / 87178291200.0);
+  p = fma(p, r, 1.0 / 6227020800.0);
+  p = fma(p, r, 1.0 / 479001600.0);
+  p = fma(p, r, 1.0 / 39916800.0);
+  p = fma(p, r, 1.0 / 3628800.0);
+  p = fma(p, r, 1.0 / 362880.0);
+  p = fma(p, r, 1.0 / 40320.0);
+  p = fma(p, r, 1.0 / 5040.0);
+  p = fma(p, r, 1.0 / 720.0);
+  p = fma(p, r, 1.0 / 120.0);
+  p = fma(p, r, 1.0 / 24.0);
+  p = fma(p, r, 1.0 / 6.0);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  const int ki = (int)k;
+  const int k1 = ki / 2, k2 = ki - k1;
+  const double s1 = __longlong_as_double((long long)((uint64_t)(k1 + 1023) << 52));
+  const double s2 = __longlong_as_double((long long)((uint64_t)(k2 + 1023) << 52));
+  return (p * s1) * s2;
+}
+__device__ inline double pow_d(double x, double y) {
+  if (y == 0.0) return 1.0;
+  if (x == 0.0) return y > 0 ? 0.0 : __builtin_inf();
+  return exp_d(y * log_d(x));
+}
+__device__ inline float pow_f(float x, float y) {  // C powf semantics
+  if (y == 0.f) return 1.f;
+  if (x == 0.f) return y > 0.f ? 0.f : __builtin_inff();
+  if (x < 0.f) {
+    if (floorf(y) != y) return __builtin_nanf("");
+    const float r = (float)pow_d(-(double)x, (double)y);
+    const double half = (double)y * 0.5;
+    return (floor(half) != half) ? -r : r;
+  }
+  return (float)pow_d((double)x, (double)y);
+}
+
+// ------------------------------------------------------------ fp32 vectors
+struct V3 {
+  float x, y, z;
+};
+__device__ __forceinline__ V3 mk(float x, float y, float z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 sub(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ float dot3(V3 a, V3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+__device__ __forceinline__ V3 cross3(V3 a, V3 b) {
+  return mk(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
+}
+__device__ __forceinline__ V3 unit(V3 v) {
+  const float n2 = dot3(v, v);
+  if (n2 > 0.f) {
+    const float s = sqrtf(n2);
+    v = mk(v.x / s, v.y / s, v.z / s);
+  }
+  return v;
+}
+__device__ __forceinline__ V3 along(V3 p, V3 d, float t) {
+  return mk(fmaf(d.x, t, p.x), fmaf(d.y, t, p.y), fmaf(d.z, t, p.z));
+}
+
+// ------------------------------------------------------------ closest hit
+// Object::getIntersection (scene_basics.h:426-459) over every triangle in
+// object order (BVH::getIntersection with its single leaf, bvh.h:55-77):
+// strict '<' keeps the first of equal-t hits.  The triangle loop is wave-
+// uniform, so the 80-B records come in through scalar loads; the test is
+// evaluated branch-free per lane and committed with a select.  Each skip
+// condition is written exactly as the reference's (negated) so NaNs take the
+// same branch.
+__device__ __forceinline__ int closest_hit(const TriIsect *__restrict__ tris, int nT, V3 p, V3 d,
+                                           float &best_t) {
+  float bt = __builtin_inff();
+  int bi = -1;
+#pragma unroll 2
+  for (int i = 0; i < nT; ++i) {
+    const TriIsect T = tris[i];
+    const float denom = fmaf(T.n[2], d.z, fmaf(T.n[1], d.y, T.n[0] * d.x));
+    const float px = p.x - T.c[0], py = p.y - T.c[1], pz = p.z - T.c[2];
+    const float num = fmaf(pz, T.n[2], fmaf(py, T.n[1], px * T.n[0]));
+    const float t = num / -denom;
+    const float qx = fmaf(d.x, t, p.x), qy = fmaf(d.y, t, p.y), qz = fmaf(d.z, t, p.z);
+    const float s0 = fmaf(qz, T.e0[2], fmaf(qy, T.e0[1], fmaf(qx, T.e0[0], T.e0[3])));
+    const float s1 = fmaf(qz, T.e1[2], fmaf(qy, T.e1[1], fmaf(qx, T.e1[0], T.e1[3])));
+    const float s2 = fmaf(qz, T.e2[2], fmaf(qy, T.e2[1], fmaf(qx, T.e2[0], T.e2[3])));
+    const bool take = !(fabsf(denom) < kMinDotUp) && !(t < kEpsUp) && !(t >= bt) && !(s0 > 0.f) &&
+                      !(s1 > 0.f) && !(s2 > 0.f);
+    bt = take ? t : bt;
+    bi = take ? i : bi;
+  }
+  best_t = bt;
+  return bi;
+}
+
+// Triangle::getNormal (scene_basics.h:100-109)
+__device__ __forceinline__ V3 shading_normal(const TriGeom &g, V3 q) {
+  const V3 v0 = mk(g.v[0][0], g.v[0][1], g.v[0][2]);
+  const V3 v1 = mk(g.v[1][0], g.v[1][1], g.v[1][2]);
+  const V3 v2 = mk(g.v[2][0], g.v[2][1], g.v[2][2]);
+  const V3 c0 = cross3(sub(v1, q), sub(v2, q));
+  const V3 c1 = cross3(sub(v2, q), sub(v0, q));
+  const V3 c2 = cross3(sub(v0, q), sub(v1, q));
+  const float w0 = (0.5f * sqrtf(dot3(c0, c0))) / g.area;
+  const float w1 = (0.5f * sqrtf(dot3(c1, c1))) / g.area;
+  const float w2 = (0.5f * sqrtf(dot3(c2, c2))) / g.area;
+  const V3 n = mk(fmaf(g.vn[2][0], w2, fmaf(g.vn[1][0], w1, g.vn[0][0] * w0)),
+                  fmaf(g.vn[2][1], w2, fmaf(g.vn[1][1], w1, g.vn[0][1] * w0)),
+                  fmaf(g.vn[2][2], w2, fmaf(g.vn[1][2], w1, g.vn[0][2] * w0)));
+  return unit(n);
+}
+
+// Camera ray (path_trace.cu:155-165) + Ray::transform (scene_basics.h:307-319)
+__device__ __forceinline__ void camera_ray(const float *cam, Rng &st, int r, int c, int W, int H, V3 &p,
+                                           V3 &d) {
+  const float u0 = uniform(st), u1 = uniform(st);
+  const float x = 2.f * ((float)c + u0) / (float)W - 1.f;
+  const float y = 1.f - 2.f * ((float)r + u1) / (float)H;
+  const V3 d0 = unit(mk(x, y, 1.f));
+  float pr[3], dr[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float *M = cam + 4 * i;
+    pr[i] = fmaf(M[3], 1.f, fmaf(M[2], 0.f, fmaf(M[1], 0.f, M[0] * 0.f)));
+    dr[i] = fmaf(M[3], 0.f, fmaf(M[2], d0.z, fmaf(M[1], d0.y, M[0] * d0.x)));
+  }
+  p = mk(pr[0], pr[1], pr[2]);
+  d = unit(mk(dr[0], dr[1], dr[2]));
+}
+
+// Phong lobe of BSDF (path_trace.cu:19-22)
+__device__ inline float phong(float shin, V3 nrm, V3 w, V3 wi) {
+  const float dn = dot3(nrm, wi);
+  const V3 refl = mk(fmaf(2.f * dn, nrm.x, -wi.x), fmaf(2.f * dn, nrm.y, -wi.y), fmaf(2.f * dn, nrm.z, -wi.z));
+  const float pw = pow_f(dot3(refl, w), shin);
+  const float mx = pw > 0.f ? pw : 0.f;
+  return (float)((((double)(shin + 2.f)) / 2.0 / kPi) * (double)mx);
+}
+
+}  // namespace dev
+}  // namespace ipt

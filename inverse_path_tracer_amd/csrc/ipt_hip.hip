@@ -1,0 +1,688 @@
+// ipt_hip.hip -- MI355X (gfx950) kernels of the inverse path tracer.
+//
+// One persistent megakernel traces paths for three integrators that share the
+// reference's sampling (template MODE):
+//   MODE_FWD    path_trace.cu:111-184  (renderSample/radiance): per-sample
+//               radiance to a sample buffer, then pixel_mean_kernel
+//               (path_trace.cu:186-198 toneMap) averages it;
+//   MODE_ADJ    new: dLoss/dKd of the same estimator under common random
+//               numbers (path replay with per-lane vertex records in LDS and
+//               a backward sweep when the path ends);
+//   MODE_GRAPH  inv_path_trace.cu:109-191 (createGraph): triangle->triangle
+//               transport edges accumulated in LDS-privatised fp64 bins.
+//
+// MI355X-first structure:
+//   * one ray per lane, 256-thread workgroups, a grid of exactly the resident
+//     workgroups (persistent); each wave owns a contiguous range of global
+//     sample indices and refills finished lanes from it with
+//     ballot + mbcnt (wave-level compaction, no atomics), so lanes stay busy
+//     whatever the path-length spread (the reference's one-thread-per-sample
+//     launch idles a wave until its longest path ends);
+//   * every loop iteration casts exactly ONE ray per active lane (path rays
+//     and next-event shadow rays are phases of one state machine), so the
+//     dominant cost -- the closest-hit loop -- always runs with full waves;
+//   * the closest-hit loop walks the triangle table with a wave-uniform
+//     index: 80-B records arrive through scalar loads and the test is
+//     branch-free per lane.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "gpu_api.h"
+#include "ipt_device.h"
+
+namespace ipt {
+
+static thread_local std::string g_gpu_err;
+void gpu_set_error(const std::string &e) { g_gpu_err = e; }
+const char *gpu_last_error() { return g_gpu_err.c_str(); }
+
+#define HIP_TRY(expr)                                                                        \
+  do {                                                                                       \
+    hipError_t e_ = (expr);                                                                  \
+    if (e_ != hipSuccess) {                                                                  \
+      gpu_set_error(std::string(#expr) + ": " + hipGetErrorString(e_));                      \
+      return -1;                                                                             \
+    }                                                                                        \
+  } while (0)
+
+enum { MODE_FWD = 0, MODE_ADJ = 1, MODE_GRAPH = 2 };
+enum { PHASE_PATH = 0, PHASE_SHADOW = 1 };
+constexpr int kBlock = 256;
+constexpr int kRecFields = 7;  // adjoint vertex record: tri, lo[3], specd, coeff, speci
+constexpr int kEdgeW = 8;      // graph bin: w, w*f, pix[3]*w*f, light[3]*w*f
+constexpr int kMaxAdjBounces = 62;
+
+struct TraceArgs {
+  int W, H, spp, max_bounces;
+  uint64_t seed;
+  uint64_t s_begin, n_samples;
+  int nT, nE;
+  int lds_edges;  // GRAPH: bins privatised in LDS
+  float cam[16];
+};
+
+using namespace dev;
+
+// ---------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void trace_kernel(
+    const TriIsect *__restrict__ isect, const TriGeom *__restrict__ geom, const TriMat *__restrict__ mat,
+    const float *__restrict__ kd, const int *__restrict__ emit_tri, const float *__restrict__ emit_cdf,
+    const float *__restrict__ emit_pmf, const TraceArgs a, float *__restrict__ out_samples,
+    const float *__restrict__ adj, double *__restrict__ grad, const uint8_t *__restrict__ target,
+    double *__restrict__ edges) {
+  extern __shared__ double lds[];
+  const int tid = threadIdx.x;
+  const int nT = a.nT, nE = a.nE;
+  const int vmax = a.max_bounces + 1;  // ADJ record capacity per lane
+  double *lds_acc = lds;               // ADJ: nT*3 grad; GRAPH: (nT+1)*nT*kEdgeW bins
+  float *lds_rec = nullptr;
+  int n_acc = 0;
+  if (MODE == MODE_ADJ) {
+    n_acc = nT * 3;
+    lds_rec = reinterpret_cast<float *>(lds + n_acc);
+  } else if (MODE == MODE_GRAPH && a.lds_edges) {
+    n_acc = (nT + 1) * nT * kEdgeW;
+  }
+  for (int i = tid; i < n_acc; i += kBlock) lds_acc[i] = 0.0;
+  if (MODE != MODE_FWD) __syncthreads();
+  double *acc = (MODE == MODE_GRAPH && !a.lds_edges) ? edges : lds_acc;
+
+  // wave-uniform sample range (static partition, regenerated per lane)
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * kBlock + tid) >> 6);
+  const uint32_t nwaves = (gridDim.x * kBlock) >> 6;
+  uint64_t next = a.s_begin + (a.n_samples * wave) / nwaves;
+  const uint64_t end = a.s_begin + (a.n_samples * (wave + 1)) / nwaves;
+
+  bool active = false;
+  Rng st;
+  V3 p = mk(0.f, 0.f, 0.f), d = p, nh = p, din = p;
+  V3 L = p, Le = p, Ld = p, M = mk(1.f, 1.f, 1.f);
+  V3 lo = p;              // ADJ: Ke*s of the current vertex
+  float specd = 0.f, ct = 0.f;
+  float weight = 1.f;     // GRAPH path weight
+  V3 pix = p;             // GRAPH target pixel
+  int tri = -1, emitter = 0, k = 0, phase = PHASE_PATH, dst = 0;
+  uint64_t gidx = 0;
+
+  for (;;) {
+    // ---- refill finished lanes from the wave's range (ballot + mbcnt)
+    const uint64_t need = __ballot(!active);
+    if (need) {
+      const uint32_t rank =
+          __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+      if (!active) {
+        const uint64_t g = next + rank;
+        if (g < end) {
+          gidx = g;
+          rng_init(st, a.seed + g);
+          const uint64_t pixel = g / (uint64_t)a.spp;
+          const int r = (int)(pixel / (uint64_t)a.W), c = (int)(pixel % (uint64_t)a.W);
+          camera_ray(a.cam, st, r, c, a.W, a.H, p, d);
+          L = mk(0.f, 0.f, 0.f);
+          Le = L;
+          Ld = L;
+          M = mk(1.f, 1.f, 1.f);
+          k = 0;
+          phase = PHASE_PATH;
+          if (MODE == MODE_GRAPH) {
+            weight = 1.f;
+            dst = nT;
+            const uint8_t *px = target + ((size_t)r * a.W + c) * 3;
+            pix = mk((float)px[0] / 255.0f, (float)px[1] / 255.0f, (float)px[2] / 255.0f);
+          }
+          active = true;
+        }
+      }
+      next += (uint64_t)__popcll(need);
+    }
+    if (__ballot(active) == 0) break;
+    if (!active) continue;
+
+    // ---- exactly one ray per active lane
+    float t;
+    const int hit = closest_hit(isect, nT, p, d, t);
+
+    bool after_nee = false, finished = false, escaped = false;
+    if (phase == PHASE_PATH) {
+      if (hit < 0) {
+        finished = true;
+        escaped = (k > 0);
+        if (MODE != MODE_GRAPH) {
+          L = mk(fmaf(M.x, Le.x + Ld.x, L.x), fmaf(M.y, Le.y + Ld.y, L.y), fmaf(M.z, Le.z + Ld.z, L.z));
+        }
+      } else {
+        tri = hit;
+        const V3 q = along(p, d, t);
+        if (MODE == MODE_GRAPH) {
+          (void)uniform(st);  // isSpecular = u < P_SPEC(0), inv_path_trace.cu:117
+          double *e = acc + ((size_t)dst * nT + tri) * kEdgeW;  // Edge::update, inv_scene.h:26-36
+          const float wf = weight * 1.f;
+          atomicAdd(e + 0, (double)weight);
+          atomicAdd(e + 1, (double)wf);
+          atomicAdd(e + 2, (double)(wf * pix.x));
+          atomicAdd(e + 3, (double)(wf * pix.y));
+          atomicAdd(e + 4, (double)(wf * pix.z));
+        } else if (k == 0) {
+          const TriMat &m = mat[tri];
+          Le = mk(m.ke[0], m.ke[1], m.ke[2]);
+        }
+        nh = shading_normal(geom[tri], q);
+        din = d;
+        p = q;
+        Ld = mk(0.f, 0.f, 0.f);
+        lo = Ld;
+        specd = 0.f;
+        if (nE > 0) {  // directLighting, path_trace.cu:30-89
+          const float u = uniform(st);
+          int ie = 0;
+          while (ie < nE && !(emit_cdf[ie] >= u)) ++ie;
+          ie = ie < nE ? ie : nE - 1;
+          const float r1 = uniform(st), r2 = uniform(st);
+          const double sq = sqrt((double)r1);
+          const float ca = (float)(1.0 - sq);
+          const float cb = (float)(sq * (double)(1.f - r2));
+          const float cc = (float)((double)r2 * sq);
+          const TriGeom &ge = geom[emit_tri[ie]];
+          const V3 pt = mk(fmaf(cc, ge.v[2][0], fmaf(cb, ge.v[1][0], ca * ge.v[0][0])),
+                           fmaf(cc, ge.v[2][1], fmaf(cb, ge.v[1][1], ca * ge.v[0][1])),
+                           fmaf(cc, ge.v[2][2], fmaf(cb, ge.v[1][2], ca * ge.v[0][2])));
+          const V3 tl = unit(sub(pt, q));
+          const float cth = dot3(nh, tl);
+          if (cth < 0.f) {
+            after_nee = true;
+          } else {
+            d = tl;
+            ct = cth;
+            emitter = ie;
+            phase = PHASE_SHADOW;
+          }
+        } else {
+          after_nee = true;
+        }
+      }
+    } else {  // shadow ray of next-event estimation
+      phase = PHASE_PATH;
+      after_nee = true;
+      const int et = emit_tri[emitter];
+      if (hit == et) {
+        const V3 qs = along(p, d, t);
+        const V3 ne = shading_normal(geom[et], qs);
+        const float ctp = -dot3(ne, d);
+        if (!(ctp < 0.f)) {
+          const double td = (double)t;
+          const TriMat &me = mat[et];
+          if (MODE == MODE_GRAPH) {
+            const float w2 =
+                (float)(((double)((weight * ct) * ctp) / (td * td)) / (double)emit_pmf[emitter]);
+            double *e = acc + ((size_t)tri * nT + et) * kEdgeW;
+            const float wf = w2 * kInvPiF;  // BSDF(direct) factor 1/pi, inv_path_trace.cu:8
+            atomicAdd(e + 0, (double)w2);
+            atomicAdd(e + 1, (double)wf);
+            atomicAdd(e + 2, (double)(wf * pix.x));
+            atomicAdd(e + 3, (double)(wf * pix.y));
+            atomicAdd(e + 4, (double)(wf * pix.z));
+            atomicAdd(e + 5, (double)(wf * me.ke[0]));
+            atomicAdd(e + 6, (double)(wf * me.ke[1]));
+            atomicAdd(e + 7, (double)(wf * me.ke[2]));
+          } else {
+            const float s = (float)(((double)(ct * ctp) / (td * td)) / (double)emit_pmf[emitter]);
+            lo = mk(me.ke[0] * s, me.ke[1] * s, me.ke[2] * s);
+            const TriMat &m = mat[tri];
+            if (m.flags & MAT_HAS_KS) specd = phong(m.shininess, nh, din, d);
+            const float *kdt = kd + 3 * tri;
+            Ld = mk((kdt[0] + m.ks[0] * specd) * lo.x, (kdt[1] + m.ks[1] * specd) * lo.y,
+                    (kdt[2] + m.ks[2] * specd) * lo.z);
+          }
+        }
+      }
+    }
+
+    if (after_nee) {
+      bool cont = false;
+      const V3 Mp = M;
+      float coeff = 0.f, speci = 0.f;
+      if (!(a.max_bounces >= 0 && k == a.max_bounces)) {
+        const float pr = uniform(st);  // Russian roulette, path_trace.cu:130-131
+        if (pr < kPRR) {
+          // sampleNextDir, path_trace.cu:91-109
+          const TriMat &m = mat[tri];
+          const bool spec = (MODE != MODE_GRAPH) && (m.flags & MAT_SPECULAR);
+          const float uphi = uniform(st);
+          const float phi = (float)(2.0 * kPi * (double)uphi);
+          const float ut = uniform(st);
+          float cth, sth, psamp;
+          if (!spec) {
+            cth = (float)sqrt((double)ut);
+            sth = (float)sqrt(1.0 - (double)ut);
+            psamp = kInvPiF;
+          } else {
+            const double cd = pow_d((double)ut, 1.0 / ((double)m.shininess + 1.0));
+            cth = (float)cd;
+            sth = (float)sqrt(1.0 - cd * cd);
+            psamp = pow_f((m.shininess + 1.f) * cth, m.shininess);
+          }
+          float sp, cp;
+          sincos_f(phi, sp, cp);
+          const V3 h = mk(sth * cp, sth * sp, cth);
+          const TriGeom &g = geom[tri];
+          const V3 nd = unit(mk(fmaf(g.R[0][2], h.z, fmaf(g.R[0][1], h.y, g.R[0][0] * h.x)),
+                                fmaf(g.R[1][2], h.z, fmaf(g.R[1][1], h.y, g.R[1][0] * h.x)),
+                                fmaf(g.R[2][2], h.z, fmaf(g.R[2][1], h.y, g.R[2][0] * h.x))));
+          if (MODE == MODE_GRAPH) {
+            weight *= dot3(nd, nh);  // inv_path_trace.cu:144-145
+            weight = (float)((double)weight * (((1.0 / (double)kInvPiF) / (double)kPRR) / 1.0));
+            dst = tri;
+          } else {
+            if (m.flags & MAT_HAS_KS) speci = phong(m.shininess, nh, din, nd);
+            coeff = (dot3(nd, nh) / psamp) / kPRR;
+            const float *kdt = kd + 3 * tri;
+            M = mk((M.x * (kdt[0] / kPiF + m.ks[0] * speci)) * coeff,
+                   (M.y * (kdt[1] / kPiF + m.ks[1] * speci)) * coeff,
+                   (M.z * (kdt[2] / kPiF + m.ks[2] * speci)) * coeff);
+          }
+          d = nd;
+          cont = true;
+        }
+      }
+      if (MODE == MODE_ADJ) {  // vertex record k (layout [field][vertex][lane])
+        float *rec = lds_rec + (size_t)k * kBlock + tid;
+        const size_t fs = (size_t)vmax * kBlock;
+        rec[0] = __int_as_float(tri);
+        rec[fs] = lo.x;
+        rec[2 * fs] = lo.y;
+        rec[3 * fs] = lo.z;
+        rec[4 * fs] = specd;
+        rec[5 * fs] = coeff;
+        rec[6 * fs] = speci;
+      }
+      if (MODE != MODE_GRAPH) {
+        L = mk(fmaf(Mp.x, Le.x + Ld.x, L.x), fmaf(Mp.y, Le.y + Ld.y, L.y), fmaf(Mp.z, Le.z + Ld.z, L.z));
+      }
+      if (cont) {
+        ++k;
+      } else {
+        finished = true;
+        ++k;  // vertices recorded = k
+      }
+    }
+
+    if (finished) {
+      active = false;
+      if (MODE == MODE_FWD) {
+        float *o = out_samples + (gidx - a.s_begin) * 3;
+        o[0] = L.x;
+        o[1] = L.y;
+        o[2] = L.z;
+      } else if (MODE == MODE_ADJ) {
+        // backward sweep over the recorded vertices (oracle adjoint_sample)
+        const int K = k;
+        if (K > 0) {
+          const size_t fs = (size_t)vmax * kBlock;
+          const uint64_t pixel = gidx / (uint64_t)a.spp;
+          const float ax = adj[pixel * 3 + 0] / (float)a.spp;
+          const float ay = adj[pixel * 3 + 1] / (float)a.spp;
+          const float az = adj[pixel * 3 + 2] / (float)a.spp;
+          V3 S = mk(0.f, 0.f, 0.f);
+          if (escaped) {
+            const float *r = lds_rec + (size_t)(K - 1) * kBlock + tid;
+            const int tk = __float_as_int(r[0]);
+            const float sd = r[4 * fs];
+            const TriMat &m = mat[tk];
+            const float *kdt = kd + 3 * tk;
+            S = mk(Le.x + (kdt[0] + m.ks[0] * sd) * r[fs], Le.y + (kdt[1] + m.ks[1] * sd) * r[2 * fs],
+                   Le.z + (kdt[2] + m.ks[2] * sd) * r[3 * fs]);
+          }
+          for (int kk = K - 1; kk >= 0; --kk) {
+            // prefix throughput M_kk (recomputed exactly as the forward did)
+            V3 Mk = mk(1.f, 1.f, 1.f);
+            for (int j = 0; j < kk; ++j) {
+              const float *rj = lds_rec + (size_t)j * kBlock + tid;
+              const int tj = __float_as_int(rj[0]);
+              const float cj = rj[5 * fs], sj = rj[6 * fs];
+              const TriMat &mj = mat[tj];
+              const float *kdj = kd + 3 * tj;
+              Mk = mk((Mk.x * (kdj[0] / kPiF + mj.ks[0] * sj)) * cj, (Mk.y * (kdj[1] / kPiF + mj.ks[1] * sj)) * cj,
+                      (Mk.z * (kdj[2] / kPiF + mj.ks[2] * sj)) * cj);
+            }
+            const float *r = lds_rec + (size_t)kk * kBlock + tid;
+            const int tk = __float_as_int(r[0]);
+            const V3 lk = mk(r[fs], r[2 * fs], r[3 * fs]);
+            const float sd = r[4 * fs], ck = r[5 * fs], si = r[6 * fs];
+            const bool last_esc = escaped && kk == K - 1;
+            const bool continued = (kk < K - 1) || escaped;
+            V3 dLd = Mk;
+            if (last_esc) dLd = mk(dLd.x + M.x, dLd.y + M.y, dLd.z + M.z);
+            V3 gk = mk(dLd.x * lk.x, dLd.y * lk.y, dLd.z * lk.z);
+            if (continued) {
+              const float cpi = ck / kPiF;
+              gk = mk(gk.x + (cpi * Mk.x) * S.x, gk.y + (cpi * Mk.y) * S.y, gk.z + (cpi * Mk.z) * S.z);
+            }
+            atomicAdd(&lds_acc[tk * 3 + 0], (double)(ax * gk.x));
+            atomicAdd(&lds_acc[tk * 3 + 1], (double)(ay * gk.y));
+            atomicAdd(&lds_acc[tk * 3 + 2], (double)(az * gk.z));
+            const TriMat &m = mat[tk];
+            const float *kdt = kd + 3 * tk;
+            S = mk((Le.x + (kdt[0] + m.ks[0] * sd) * lk.x) + ((kdt[0] / kPiF + m.ks[0] * si) * ck) * S.x,
+                   (Le.y + (kdt[1] + m.ks[1] * sd) * lk.y) + ((kdt[1] / kPiF + m.ks[1] * si) * ck) * S.y,
+                   (Le.z + (kdt[2] + m.ks[2] * sd) * lk.z) + ((kdt[2] / kPiF + m.ks[2] * si) * ck) * S.z);
+          }
+        }
+      }
+    }
+  }
+
+  if (MODE != MODE_FWD) {
+    __syncthreads();
+    if (!(MODE == MODE_GRAPH && !a.lds_edges)) {
+      double *dstp = (MODE == MODE_ADJ) ? grad : edges;
+      for (int i = tid; i < n_acc; i += kBlock) {
+        const double v = lds_acc[i];
+        if (v != 0.0) atomicAdd(dstp + i, v);
+      }
+    }
+  }
+}
+
+// toneMap, path_trace.cu:186-198: sequential divide-then-sum per pixel.
+__global__ __launch_bounds__(kBlock) void pixel_mean_kernel(const float *__restrict__ samples, int64_t npix,
+                                                            int spp, float *__restrict__ hdr,
+                                                            uint8_t *__restrict__ ldr) {
+  const int64_t px = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (px >= npix) return;
+  const float *s = samples + px * spp * 3;
+  float tx = 0.f, ty = 0.f, tz = 0.f;
+  const float fs = (float)spp;
+  for (int i = 0; i < spp; ++i) {
+    tx += s[3 * i] / fs;
+    ty += s[3 * i + 1] / fs;
+    tz += s[3 * i + 2] / fs;
+  }
+  hdr[px * 3] = tx;
+  hdr[px * 3 + 1] = ty;
+  hdr[px * 3 + 2] = tz;
+  if (ldr) {
+    ldr[px * 3] = (uint8_t)(255.f * tx / (1 + tx));
+    ldr[px * 3 + 1] = (uint8_t)(255.f * ty / (1 + ty));
+    ldr[px * 3 + 2] = (uint8_t)(255.f * tz / (1 + tz));
+  }
+}
+
+// ---------------------------------------------------------------------------
+struct GpuScene {
+  HostScene host;
+  int device = 0;
+  bool on_device = false;
+  TriIsect *isect = nullptr;
+  TriGeom *geom = nullptr;
+  TriMat *mat = nullptr;
+  float *kd = nullptr;
+  int *emit_tri = nullptr;
+  float *emit_cdf = nullptr, *emit_pmf = nullptr;
+  float *ws = nullptr;  // per-sample radiance workspace
+  size_t ws_bytes = 0;
+  int grid[3] = {0, 0, 0};  // resident workgroups per mode (0 = not queried)
+  size_t grid_lds[3] = {0, 0, 0};
+};
+
+const HostScene &gpu_host(const GpuScene *s) { return s->host; }
+HostScene &gpu_host_mut(GpuScene *s) { return s->host; }
+
+template <typename T>
+static int upload(T **dst, const std::vector<T> &v) {
+  const size_t n = std::max<size_t>(v.size(), 1) * sizeof(T);
+  HIP_TRY(hipMalloc(reinterpret_cast<void **>(dst), n));
+  if (!v.empty()) HIP_TRY(hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return 0;
+}
+
+GpuScene *gpu_upload(const HostScene &host, std::string *err) {
+  GpuScene *s = new GpuScene();
+  s->host = host;
+  if (hipGetDevice(&s->device) != hipSuccess) {
+    *err = "no HIP device available";
+    delete s;
+    return nullptr;
+  }
+  if (upload(&s->isect, host.isect) || upload(&s->geom, host.geom) || upload(&s->mat, host.mat) ||
+      upload(&s->kd, host.kd) || upload(&s->emit_tri, host.emit_tri) || upload(&s->emit_cdf, host.emit_cdf) ||
+      upload(&s->emit_pmf, host.emit_pmf)) {
+    *err = gpu_last_error();
+    gpu_free(s);
+    return nullptr;
+  }
+  s->on_device = true;
+  return s;
+}
+
+GpuScene *gpu_host_only(const HostScene &host) {
+  GpuScene *s = new GpuScene();
+  s->host = host;
+  return s;
+}
+bool gpu_on_device(const GpuScene *s) { return s->on_device; }
+
+void gpu_free(GpuScene *s) {
+  if (!s) return;
+  if (!s->on_device) {
+    delete s;
+    return;
+  }
+  (void)hipFree(s->isect);
+  (void)hipFree(s->geom);
+  (void)hipFree(s->mat);
+  (void)hipFree(s->kd);
+  (void)hipFree(s->emit_tri);
+  (void)hipFree(s->emit_cdf);
+  (void)hipFree(s->emit_pmf);
+  (void)hipFree(s->ws);
+  delete s;
+}
+
+int gpu_set_kd(GpuScene *s, const float *kd_host) {
+  std::memcpy(s->host.kd.data(), kd_host, s->host.kd.size() * sizeof(float));
+  if (!s->on_device) return 0;
+  HIP_TRY(hipMemcpy(s->kd, kd_host, s->host.kd.size() * sizeof(float), hipMemcpyHostToDevice));
+  return 0;
+}
+
+int gpu_device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+static int check_params(const GpuScene *s, const RenderParams &p) {
+  if (!s->on_device) {
+    gpu_set_error("scene was loaded host-only (ipt_load_scene_host); it cannot be rendered");
+    return -1;
+  }
+  if (p.width <= 0 || p.height <= 0 || p.spp <= 0 || p.row_begin < 0 || p.row_end > p.height ||
+      p.row_begin > p.row_end) {
+    gpu_set_error("invalid render parameters (width/height/spp > 0, 0 <= row_begin <= row_end <= height)");
+    return -1;
+  }
+  if ((uint64_t)p.width * (uint64_t)p.height * (uint64_t)p.spp >= (1ull << 40)) {
+    gpu_set_error("too many samples (width*height*spp must be < 2^40)");
+    return -1;
+  }
+  if (s->host.nT <= 0) {
+    gpu_set_error("scene has no triangles");
+    return -1;
+  }
+  return 0;
+}
+
+template <int MODE>
+static int resident_grid(GpuScene *s, size_t lds_bytes, int *grid) {
+  if (s->grid[MODE] == 0 || s->grid_lds[MODE] != lds_bytes) {
+    int per_cu = 0, cus = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<MODE>, kBlock, lds_bytes));
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device));
+    if (per_cu <= 0) {
+      gpu_set_error("trace kernel cannot be resident (LDS request too large?)");
+      return -1;
+    }
+    s->grid[MODE] = per_cu * cus;
+    s->grid_lds[MODE] = lds_bytes;
+  }
+  *grid = s->grid[MODE];
+  return 0;
+}
+
+static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
+  TraceArgs a;
+  a.W = p.width;
+  a.H = p.height;
+  a.spp = p.spp;
+  a.max_bounces = p.max_bounces < 0 ? -1 : p.max_bounces;
+  a.seed = p.seed;
+  a.s_begin = (uint64_t)p.row_begin * p.width * p.spp;
+  a.n_samples = (uint64_t)(p.row_end - p.row_begin) * p.width * p.spp;
+  a.nT = s->host.nT;
+  a.nE = s->host.nE;
+  a.lds_edges = 0;
+  std::memcpy(a.cam, s->host.cam, sizeof a.cam);
+  return a;
+}
+
+template <int MODE>
+static int launch(GpuScene *s, const TraceArgs &a, size_t lds, const float *kd_dev, float *out, const float *adj,
+                  double *grad, const uint8_t *target, double *edges, hipStream_t st) {
+  int grid = 0;
+  if (resident_grid<MODE>(s, lds, &grid)) return -1;
+  if (a.n_samples == 0) return 0;
+  hipLaunchKernelGGL(trace_kernel<MODE>, dim3(grid), dim3(kBlock), lds, st, s->isect, s->geom, s->mat,
+                     kd_dev ? kd_dev : s->kd, s->emit_tri, s->emit_cdf, s->emit_pmf, a, out, adj, grad, target,
+                     edges);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int gpu_render_samples(GpuScene *s, const RenderParams &p, const float *kd_dev, float *samples_dev, void *stream) {
+  if (check_params(s, p)) return -1;
+  const TraceArgs a = make_args(s, p);
+  return launch<MODE_FWD>(s, a, 0, kd_dev, samples_dev, nullptr, nullptr, nullptr, nullptr, (hipStream_t)stream);
+}
+
+int gpu_pixel_mean(const float *samples_dev, int64_t npix, int spp, float *hdr_dev, uint8_t *ldr_dev, void *stream) {
+  if (npix <= 0) return 0;
+  const int blocks = (int)((npix + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(pixel_mean_kernel, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, samples_dev, npix, spp,
+                     hdr_dev, ldr_dev);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+static int ensure_ws(GpuScene *s, size_t bytes) {
+  if (bytes > s->ws_bytes) {
+    if (s->ws) HIP_TRY(hipFree(s->ws));
+    s->ws = nullptr;
+    s->ws_bytes = 0;
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s->ws), bytes));
+    s->ws_bytes = bytes;
+  }
+  return 0;
+}
+
+int gpu_render(GpuScene *s, const RenderParams &p, const float *kd_dev, float *hdr_dev, uint8_t *ldr_dev,
+               void *stream) {
+  if (check_params(s, p)) return -1;
+  const int64_t npix = (int64_t)(p.row_end - p.row_begin) * p.width;
+  if (ensure_ws(s, (size_t)npix * p.spp * 3 * sizeof(float))) return -1;
+  if (gpu_render_samples(s, p, kd_dev, s->ws, stream)) return -1;
+  return gpu_pixel_mean(s->ws, npix, p.spp, hdr_dev, ldr_dev, stream);
+}
+
+int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const float *adj_dev, double *grad_dev,
+                void *stream) {
+  if (check_params(s, p)) return -1;
+  if (p.max_bounces < 0 || p.max_bounces > kMaxAdjBounces) {
+    gpu_set_error("adjoint requires 0 <= max_bounces <= 62 (vertex records live in LDS)");
+    return -1;
+  }
+  const TraceArgs a = make_args(s, p);
+  const size_t lds = (size_t)s->host.nT * 3 * sizeof(double) +
+                     (size_t)(p.max_bounces + 1) * kRecFields * kBlock * sizeof(float);
+  if (lds > 160 * 1024) {
+    gpu_set_error("adjoint LDS footprint exceeds 160 KiB; lower max_bounces");
+    return -1;
+  }
+  return launch<MODE_ADJ>(s, a, lds, kd_dev, nullptr, adj_dev, grad_dev, nullptr, nullptr, (hipStream_t)stream);
+}
+
+int gpu_graph(GpuScene *s, const RenderParams &p, const uint8_t *target_dev, double *acc_dev, void *stream) {
+  if (check_params(s, p)) return -1;
+  TraceArgs a = make_args(s, p);
+  const size_t bins = (size_t)(s->host.nT + 1) * s->host.nT * kEdgeW * sizeof(double);
+  a.lds_edges = bins <= 64 * 1024 ? 1 : 0;
+  return launch<MODE_GRAPH>(s, a, a.lds_edges ? bins : 0, nullptr, nullptr, nullptr, nullptr, target_dev, acc_dev,
+                            (hipStream_t)stream);
+}
+
+// ------------------------------------------------------------ host wrappers
+namespace {
+struct DevBuf {
+  void *p = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+}  // namespace
+
+int gpu_render_samples_host(GpuScene *s, const RenderParams &p, float *samples) {
+  if (check_params(s, p)) return -1;
+  const size_t n = (size_t)(p.row_end - p.row_begin) * p.width * p.spp * 3;
+  DevBuf b;
+  HIP_TRY(hipMalloc(&b.p, std::max<size_t>(n, 1) * sizeof(float)));
+  if (gpu_render_samples(s, p, nullptr, (float *)b.p, nullptr)) return -1;
+  HIP_TRY(hipMemcpy(samples, b.p, n * sizeof(float), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int gpu_render_host(GpuScene *s, const RenderParams &p, float *hdr, uint8_t *ldr) {
+  if (check_params(s, p)) return -1;
+  const size_t npix = (size_t)(p.row_end - p.row_begin) * p.width;
+  DevBuf h, l;
+  HIP_TRY(hipMalloc(&h.p, std::max<size_t>(npix, 1) * 3 * sizeof(float)));
+  if (ldr) HIP_TRY(hipMalloc(&l.p, std::max<size_t>(npix, 1) * 3));
+  if (gpu_render(s, p, nullptr, (float *)h.p, (uint8_t *)l.p, nullptr)) return -1;
+  HIP_TRY(hipMemcpy(hdr, h.p, npix * 3 * sizeof(float), hipMemcpyDeviceToHost));
+  if (ldr) HIP_TRY(hipMemcpy(ldr, l.p, npix * 3, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int gpu_adjoint_host(GpuScene *s, const RenderParams &p, const float *adj, double *grad) {
+  if (check_params(s, p)) return -1;
+  const size_t na = (size_t)p.width * p.height * 3, ng = (size_t)s->host.nT * 3;
+  DevBuf a, g;
+  HIP_TRY(hipMalloc(&a.p, na * sizeof(float)));
+  HIP_TRY(hipMalloc(&g.p, ng * sizeof(double)));
+  HIP_TRY(hipMemcpy(a.p, adj, na * sizeof(float), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemset(g.p, 0, ng * sizeof(double)));
+  if (gpu_adjoint(s, p, nullptr, (const float *)a.p, (double *)g.p, nullptr)) return -1;
+  HIP_TRY(hipMemcpy(grad, g.p, ng * sizeof(double), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int gpu_graph_host(GpuScene *s, const RenderParams &p, const uint8_t *target, double *acc) {
+  if (check_params(s, p)) return -1;
+  const size_t nt = (size_t)p.width * p.height * 3;
+  const size_t nb = (size_t)(s->host.nT + 1) * s->host.nT * kEdgeW;
+  DevBuf t, e;
+  HIP_TRY(hipMalloc(&t.p, nt));
+  HIP_TRY(hipMalloc(&e.p, nb * sizeof(double)));
+  HIP_TRY(hipMemcpy(t.p, target, nt, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemset(e.p, 0, nb * sizeof(double)));
+  if (gpu_graph(s, p, (const uint8_t *)t.p, (double *)e.p, nullptr)) return -1;
+  HIP_TRY(hipMemcpy(acc, e.p, nb * sizeof(double), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+}  // namespace ipt

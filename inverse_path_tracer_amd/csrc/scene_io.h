@@ -1,0 +1,40 @@
+// scene_io.h -- host scene ingest: scene records -> flattened HostScene.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "scene_layout.h"
+
+namespace ipt {
+
+// One OBJECT block of a scene file (ipt_cuda.py:39-59 from_string / ObjParams).
+struct ObjectRecord {
+  float pos[3] = {0.f, 0.f, 0.f};
+  float ori[3] = {0.f, 0.f, 0.f};
+  float scl[3] = {1.f, 1.f, 1.f};
+  std::string obj_file;
+  std::string mtl_file;  // a path, or an inline "*Kd r g b*" material
+};
+
+struct HostScene {
+  int nT = 0, nE = 0;
+  std::vector<TriIsect> isect;
+  std::vector<TriGeom> geom;
+  std::vector<TriMat> mat;
+  std::vector<float> kd;        // nT*3
+  std::vector<int> emit_tri;    // nE
+  std::vector<float> emit_cdf;  // nE
+  std::vector<float> emit_pmf;  // nE
+  std::vector<int> obj_first, obj_count;
+  float cam[16];
+};
+
+// Builds the scene (scene.h:89-117 Scene::Scene semantics).  Returns false
+// and fills *err on failure (the reference exit(1)s instead).
+bool build_scene(const std::vector<ObjectRecord> &objects, HostScene *out, std::string *err);
+
+// Per-triangle export in the oracle's 57-float layout (for parity tests).
+void export_triangles(const HostScene &s, float *out);
+constexpr int kExportStride = 57;
+
+}  // namespace ipt

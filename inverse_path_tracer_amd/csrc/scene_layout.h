@@ -1,0 +1,76 @@
+// scene_layout.h -- flattened, device-resident scene layout (host + device).
+//
+// The reference keeps a pointer-rich AoS scene in CUDA managed memory
+// (Scene -> Object -> Mesh -> Triangle, scene.h:86-173, scene_basics.h:64-517)
+// and recomputes per-triangle constants inside every ray test.  Here the
+// scene is flattened once on the host into four SoA-of-records arrays that
+// are uploaded to HBM and read by the kernels:
+//
+//   TriIsect[nT]  80 B  everything the closest-hit test reads (centre,
+//                       face normal, three hoisted edge planes).  Read with a
+//                       wave-uniform index -> scalar (SMEM) loads.
+//   TriGeom[nT]  128 B  vertices, vertex normals, area, sampling frame R:
+//                       read once per path vertex by the hit lane.
+//   TriMat[nT]    32 B  Ks, shininess, Ke, flags.
+//   kd[nT*3]            diffuse albedo -- the per-material parameter vector
+//                       of getMaterials/setMaterials (scene.h:145-162); kept
+//                       separate so a torch tensor can stand in for it.
+//   emitters            global triangle index, CDF and pmf of the area-
+//                       weighted light pick (path_trace.cu:39-51).
+#pragma once
+#include <stdint.h>
+
+namespace ipt {
+
+struct TriIsect {       // 20 floats
+  float c[3];           // centre            (scene_basics.h:80-84)
+  float n[3];           // face normal       (:86-91)
+  float e0[4];          // edge plane (v0,v1): out.xyz, d  (signedDistance :497-503)
+  float e1[4];          // edge plane (v1,v2)
+  float e2[4];          // edge plane (v2,v0)
+  float pad[2];
+};
+static_assert(sizeof(TriIsect) == 80, "TriIsect layout");
+
+struct TriGeom {        // 32 floats
+  float v[3][3];        // vertices
+  float vn[3][3];       // vertex normals (columns of Triangle::normals)
+  float area;
+  float R[3][3];        // sampling frame, row-major (sampleNextDir)
+  float pad[4];
+};
+static_assert(sizeof(TriGeom) == 128, "TriGeom layout");
+
+enum : uint32_t { MAT_HAS_KS = 1u, MAT_SPECULAR = 2u };
+
+struct TriMat {         // 8 floats
+  float ks[3];
+  float shininess;
+  float ke[3];
+  uint32_t flags;
+};
+static_assert(sizeof(TriMat) == 32, "TriMat layout");
+
+// Device view of a loaded scene (all pointers are device pointers).
+struct DevScene {
+  int nT, nE;
+  const TriIsect *isect;
+  const TriGeom *geom;
+  const TriMat *mat;
+  const float *kd;
+  const int *emit_tri;
+  const float *emit_cdf;
+  const float *emit_pmf;
+  float cam[16];        // row-major 4x4 inverse view (scene.h:67-77)
+};
+
+// Explicit render parameters (the reference's compile-time constants,
+// scene.h:3-13, made run-time; defaults reproduce them).
+struct RenderParams {
+  int width, height, spp;
+  int max_bounces;      // < 0: unbounded (reference semantics)
+  uint64_t seed;
+  int row_begin, row_end;
+};
+
+}  // namespace ipt

@@ -82,9 +82,12 @@ class OracleScene:
         self.nE = L.oro_num_emissives(self.ptr)
 
     def __del__(self):
-        if getattr(self, "ptr", None):
-            lib().oro_free_scene(self.ptr)
-            self.ptr = None
+        try:
+            if getattr(self, "ptr", None) and _lib is not None:
+                _lib.oro_free_scene(self.ptr)
+                self.ptr = None
+        except Exception:
+            pass
 
     def triangles(self):
         out = np.zeros((self.nT, TRI_STRIDE), np.float32)
