@@ -194,6 +194,34 @@ __device__ __forceinline__ V3 along(V3 p, V3 d, float t) {
   return mk(fmaf(d.x, t, p.x), fmaf(d.y, t, p.y), fmaf(d.z, t, p.z));
 }
 
+// ------------------------------------------------------------ division
+// Correctly rounded a/b for the closest-hit test's operand range.  This is
+// hipcc's IEEE f32 division lowering (v_rcp + Newton + the final residual
+// fma) without v_div_scale / v_div_fixup: those only rescale operands whose
+// quotient or reciprocal would leave the normal range and patch inf/NaN/0
+// inputs.  In the hit test |b| = |n.d| lies in [1e-4, 1] and |a| <= scene
+// extent whenever the quotient is used (smaller |b| rejects the triangle
+// before t matters), so the scaling is the identity and the result equals
+// `a / b` bit for bit.  tests/test_gpu.py checks whole renders bit-exact.
+#ifndef IPT_FASTDIV
+#define IPT_FASTDIV 1
+#endif
+__device__ __forceinline__ float div_inrange(float a, float b) {
+#if IPT_FASTDIV
+  const float nb = -b;
+  const float r0 = __builtin_amdgcn_rcpf(b);
+  const float e0 = fmaf(nb, r0, 1.0f);
+  const float r1 = fmaf(e0, r0, r0);
+  const float q0 = a * r1;
+  const float e1 = fmaf(nb, q0, a);
+  const float q1 = fmaf(e1, r1, q0);
+  const float e2 = fmaf(nb, q1, a);
+  return fmaf(e2, r1, q1);
+#else
+  return a / b;
+#endif
+}
+
 // ------------------------------------------------------------ closest hit
 // Object::getIntersection (scene_basics.h:426-459) over every triangle in
 // object order (BVH::getIntersection with its single leaf, bvh.h:55-77):
@@ -202,17 +230,30 @@ __device__ __forceinline__ V3 along(V3 p, V3 d, float t) {
 // evaluated branch-free per lane and committed with a select.  Each skip
 // condition is written exactly as the reference's (negated) so NaNs take the
 // same branch.
+#ifndef IPT_PREFETCH
+#define IPT_PREFETCH 1
+#endif
 __device__ __forceinline__ int closest_hit(const TriIsect *__restrict__ tris, int nT, V3 p, V3 d,
                                            float &best_t) {
   float bt = __builtin_inff();
   int bi = -1;
+#if IPT_PREFETCH
+  // software pipeline: the scalar load of record i+1 is issued before the
+  // tests of record i (SMEM returns out of order, so every wait is a full
+  // lgkmcnt(0); issuing one record ahead hides it behind ~37 VALU ops).
+  TriIsect nxt = tris[0];
+  for (int i = 0; i < nT; ++i) {
+    const TriIsect T = nxt;
+    nxt = tris[i + 1 < nT ? i + 1 : i];
+#else
 #pragma unroll 2
   for (int i = 0; i < nT; ++i) {
     const TriIsect T = tris[i];
+#endif
     const float denom = fmaf(T.n[2], d.z, fmaf(T.n[1], d.y, T.n[0] * d.x));
     const float px = p.x - T.c[0], py = p.y - T.c[1], pz = p.z - T.c[2];
     const float num = fmaf(pz, T.n[2], fmaf(py, T.n[1], px * T.n[0]));
-    const float t = num / -denom;
+    const float t = div_inrange(num, -denom);
     const float qx = fmaf(d.x, t, p.x), qy = fmaf(d.y, t, p.y), qz = fmaf(d.z, t, p.z);
     const float s0 = fmaf(qz, T.e0[2], fmaf(qy, T.e0[1], fmaf(qx, T.e0[0], T.e0[3])));
     const float s1 = fmaf(qz, T.e1[2], fmaf(qy, T.e1[1], fmaf(qx, T.e1[0], T.e1[3])));

@@ -52,7 +52,6 @@ const char *gpu_last_error() { return g_gpu_err.c_str(); }
   } while (0)
 
 enum { MODE_FWD = 0, MODE_ADJ = 1, MODE_GRAPH = 2 };
-enum { PHASE_PATH = 0, PHASE_SHADOW = 1 };
 constexpr int kBlock = 256;
 constexpr int kRecFields = 7;  // adjoint vertex record: tri, lo[3], specd, coeff, speci
 constexpr int kEdgeW = 8;      // graph bin: w, w*f, pix[3]*w*f, light[3]*w*f
@@ -70,8 +69,16 @@ struct TraceArgs {
 using namespace dev;
 
 // ---------------------------------------------------------------------------
-template <int MODE>
-__global__ __launch_bounds__(kBlock) void trace_kernel(
+#ifndef IPT_MIN_BLOCKS
+#define IPT_MIN_BLOCKS 0
+#endif
+#if IPT_MIN_BLOCKS > 0
+#define IPT_TRACE_BOUNDS __launch_bounds__(kBlock, IPT_MIN_BLOCKS)
+#else
+#define IPT_TRACE_BOUNDS __launch_bounds__(kBlock)
+#endif
+template <int MODE, bool SPEC>
+__global__ IPT_TRACE_BOUNDS void trace_kernel(
     const TriIsect *__restrict__ isect, const TriGeom *__restrict__ geom, const TriMat *__restrict__ mat,
     const float *__restrict__ kd, const int *__restrict__ emit_tri, const float *__restrict__ emit_cdf,
     const float *__restrict__ emit_pmf, const TraceArgs a, float *__restrict__ out_samples,
@@ -102,15 +109,21 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(
 
   bool active = false;
   Rng st;
-  V3 p = mk(0.f, 0.f, 0.f), d = p, nh = p, din = p;
+  V3 p = mk(0.f, 0.f, 0.f), d = p;
   V3 L = p, Le = p, Ld = p, M = mk(1.f, 1.f, 1.f);
-  V3 lo = p;              // ADJ: Ke*s of the current vertex
-  float specd = 0.f, ct = 0.f;
-  float weight = 1.f;     // GRAPH path weight
-  V3 pix = p;             // GRAPH target pixel
-  int tri = -1, emitter = 0, k = 0, phase = PHASE_PATH, dst = 0;
+  float weight = 1.f;  // GRAPH path weight
+  V3 pix = p;          // GRAPH target pixel
+  int k = 0, dst = 0;
   uint64_t gidx = 0;
 
+  // One iteration = one path vertex for the whole wave, in two
+  // wave-synchronous phases: (1) every active lane casts its path ray and,
+  // on a hit, shades the vertex and draws ALL of the vertex's random numbers
+  // in the reference's order (NEE: emitter, r1, r2; then RR; then phi,
+  // theta); (2) the lanes that need one cast their next-event shadow ray;
+  // then every vertex lane finalises (L, M, records, next ray).  Each shading
+  // block thus runs once per vertex with most lanes on, instead of path and
+  // shadow lanes serialising each other's code every iteration.
   for (;;) {
     // ---- refill finished lanes from the wave's range (ballot + mbcnt)
     const uint64_t need = __ballot(!active);
@@ -130,7 +143,6 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(
           Ld = L;
           M = mk(1.f, 1.f, 1.f);
           k = 0;
-          phase = PHASE_PATH;
           if (MODE == MODE_GRAPH) {
             weight = 1.f;
             dst = nT;
@@ -143,117 +155,66 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(
       next += (uint64_t)__popcll(need);
     }
     if (__ballot(active) == 0) break;
-    if (!active) continue;
 
-    // ---- exactly one ray per active lane
-    float t;
-    const int hit = closest_hit(isect, nT, p, d, t);
-
-    bool after_nee = false, finished = false, escaped = false;
-    if (phase == PHASE_PATH) {
-      if (hit < 0) {
-        finished = true;
-        escaped = (k > 0);
-        if (MODE != MODE_GRAPH) {
-          L = mk(fmaf(M.x, Le.x + Ld.x, L.x), fmaf(M.y, Le.y + Ld.y, L.y), fmaf(M.z, Le.z + Ld.z, L.z));
-        }
-      } else {
-        tri = hit;
-        const V3 q = along(p, d, t);
-        if (MODE == MODE_GRAPH) {
-          (void)uniform(st);  // isSpecular = u < P_SPEC(0), inv_path_trace.cu:117
-          double *e = acc + ((size_t)dst * nT + tri) * kEdgeW;  // Edge::update, inv_scene.h:26-36
-          const float wf = weight * 1.f;
-          atomicAdd(e + 0, (double)weight);
-          atomicAdd(e + 1, (double)wf);
-          atomicAdd(e + 2, (double)(wf * pix.x));
-          atomicAdd(e + 3, (double)(wf * pix.y));
-          atomicAdd(e + 4, (double)(wf * pix.z));
-        } else if (k == 0) {
-          const TriMat &m = mat[tri];
-          Le = mk(m.ke[0], m.ke[1], m.ke[2]);
-        }
-        nh = shading_normal(geom[tri], q);
-        din = d;
-        p = q;
-        Ld = mk(0.f, 0.f, 0.f);
-        lo = Ld;
-        specd = 0.f;
-        if (nE > 0) {  // directLighting, path_trace.cu:30-89
-          const float u = uniform(st);
-          int ie = 0;
-          while (ie < nE && !(emit_cdf[ie] >= u)) ++ie;
-          ie = ie < nE ? ie : nE - 1;
-          const float r1 = uniform(st), r2 = uniform(st);
-          const double sq = sqrt((double)r1);
-          const float ca = (float)(1.0 - sq);
-          const float cb = (float)(sq * (double)(1.f - r2));
-          const float cc = (float)((double)r2 * sq);
-          const TriGeom &ge = geom[emit_tri[ie]];
-          const V3 pt = mk(fmaf(cc, ge.v[2][0], fmaf(cb, ge.v[1][0], ca * ge.v[0][0])),
-                           fmaf(cc, ge.v[2][1], fmaf(cb, ge.v[1][1], ca * ge.v[0][1])),
-                           fmaf(cc, ge.v[2][2], fmaf(cb, ge.v[1][2], ca * ge.v[0][2])));
-          const V3 tl = unit(sub(pt, q));
-          const float cth = dot3(nh, tl);
-          if (cth < 0.f) {
-            after_nee = true;
-          } else {
-            d = tl;
-            ct = cth;
-            emitter = ie;
-            phase = PHASE_SHADOW;
-          }
-        } else {
-          after_nee = true;
-        }
-      }
-    } else {  // shadow ray of next-event estimation
-      phase = PHASE_PATH;
-      after_nee = true;
-      const int et = emit_tri[emitter];
-      if (hit == et) {
-        const V3 qs = along(p, d, t);
-        const V3 ne = shading_normal(geom[et], qs);
-        const float ctp = -dot3(ne, d);
-        if (!(ctp < 0.f)) {
-          const double td = (double)t;
-          const TriMat &me = mat[et];
-          if (MODE == MODE_GRAPH) {
-            const float w2 =
-                (float)(((double)((weight * ct) * ctp) / (td * td)) / (double)emit_pmf[emitter]);
-            double *e = acc + ((size_t)tri * nT + et) * kEdgeW;
-            const float wf = w2 * kInvPiF;  // BSDF(direct) factor 1/pi, inv_path_trace.cu:8
-            atomicAdd(e + 0, (double)w2);
-            atomicAdd(e + 1, (double)wf);
-            atomicAdd(e + 2, (double)(wf * pix.x));
-            atomicAdd(e + 3, (double)(wf * pix.y));
-            atomicAdd(e + 4, (double)(wf * pix.z));
-            atomicAdd(e + 5, (double)(wf * me.ke[0]));
-            atomicAdd(e + 6, (double)(wf * me.ke[1]));
-            atomicAdd(e + 7, (double)(wf * me.ke[2]));
-          } else {
-            const float s = (float)(((double)(ct * ctp) / (td * td)) / (double)emit_pmf[emitter]);
-            lo = mk(me.ke[0] * s, me.ke[1] * s, me.ke[2] * s);
-            const TriMat &m = mat[tri];
-            if (m.flags & MAT_HAS_KS) specd = phong(m.shininess, nh, din, d);
-            const float *kdt = kd + 3 * tri;
-            Ld = mk((kdt[0] + m.ks[0] * specd) * lo.x, (kdt[1] + m.ks[1] * specd) * lo.y,
-                    (kdt[2] + m.ks[2] * specd) * lo.z);
-          }
-        }
-      }
+    // ================= phase 1: path ray (radiance, path_trace.cu:111-144)
+    float t = 0.f;
+    int hit = -1;
+    if (active) hit = closest_hit(isect, nT, p, d, t);
+    const bool vertex = active && hit >= 0;
+    bool finished = false, escaped = false;
+    if (active && hit < 0) {  // miss: the stale L_e/L_d are re-added (F4)
+      finished = true;
+      escaped = (k > 0);
+      if (MODE != MODE_GRAPH)
+        L = mk(fmaf(M.x, Le.x + Ld.x, L.x), fmaf(M.y, Le.y + Ld.y, L.y), fmaf(M.z, Le.z + Ld.z, L.z));
     }
-
-    if (after_nee) {
-      bool cont = false;
-      const V3 Mp = M;
-      float coeff = 0.f, speci = 0.f;
+    const int tri = hit;
+    V3 nh = p, din = d, sd = d, nd = d;
+    bool shadow = false, cont = false;
+    int emitter = 0;
+    float ct = 0.f, coeff = 0.f, speci = 0.f, specd = 0.f;
+    if (vertex) {
+      const V3 q = along(p, d, t);
+      if (MODE == MODE_GRAPH) {
+        (void)uniform(st);  // isSpecular = u < P_SPEC(0), inv_path_trace.cu:117
+        double *e = acc + ((size_t)dst * nT + tri) * kEdgeW;  // Edge::update, inv_scene.h:26-36
+        const float wf = weight * 1.f;
+        atomicAdd(e + 0, (double)weight);
+        atomicAdd(e + 1, (double)wf);
+        atomicAdd(e + 2, (double)(wf * pix.x));
+        atomicAdd(e + 3, (double)(wf * pix.y));
+        atomicAdd(e + 4, (double)(wf * pix.z));
+      } else if (k == 0) {
+        const TriMat &m = mat[tri];
+        Le = mk(m.ke[0], m.ke[1], m.ke[2]);
+      }
+      nh = shading_normal(geom[tri], q);
+      p = q;
+      Ld = mk(0.f, 0.f, 0.f);
+      if (nE > 0) {  // directLighting up to the shadow ray, path_trace.cu:30-71
+        const float u = uniform(st);
+        int ie = 0;
+        while (ie < nE && !(emit_cdf[ie] >= u)) ++ie;
+        ie = ie < nE ? ie : nE - 1;
+        const float r1 = uniform(st), r2 = uniform(st);
+        const double sq = sqrt((double)r1);
+        const float ca = (float)(1.0 - sq);
+        const float cb = (float)(sq * (double)(1.f - r2));
+        const float cc = (float)((double)r2 * sq);
+        const TriGeom &ge = geom[emit_tri[ie]];
+        const V3 pt = mk(fmaf(cc, ge.v[2][0], fmaf(cb, ge.v[1][0], ca * ge.v[0][0])),
+                         fmaf(cc, ge.v[2][1], fmaf(cb, ge.v[1][1], ca * ge.v[0][1])),
+                         fmaf(cc, ge.v[2][2], fmaf(cb, ge.v[1][2], ca * ge.v[0][2])));
+        sd = unit(sub(pt, q));
+        ct = dot3(nh, sd);
+        emitter = ie;
+        shadow = !(ct < 0.f);
+      }
       if (!(a.max_bounces >= 0 && k == a.max_bounces)) {
         const float pr = uniform(st);  // Russian roulette, path_trace.cu:130-131
-        if (pr < kPRR) {
-          // sampleNextDir, path_trace.cu:91-109
+        if (pr < kPRR) {                // sampleNextDir, path_trace.cu:91-109
           const TriMat &m = mat[tri];
-          const bool spec = (MODE != MODE_GRAPH) && (m.flags & MAT_SPECULAR);
+          const bool spec = SPEC && (MODE != MODE_GRAPH) && (m.flags & MAT_SPECULAR);
           const float uphi = uniform(st);
           const float phi = (float)(2.0 * kPi * (double)uphi);
           const float ut = uniform(st);
@@ -272,25 +233,58 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(
           sincos_f(phi, sp, cp);
           const V3 h = mk(sth * cp, sth * sp, cth);
           const TriGeom &g = geom[tri];
-          const V3 nd = unit(mk(fmaf(g.R[0][2], h.z, fmaf(g.R[0][1], h.y, g.R[0][0] * h.x)),
-                                fmaf(g.R[1][2], h.z, fmaf(g.R[1][1], h.y, g.R[1][0] * h.x)),
-                                fmaf(g.R[2][2], h.z, fmaf(g.R[2][1], h.y, g.R[2][0] * h.x))));
-          if (MODE == MODE_GRAPH) {
-            weight *= dot3(nd, nh);  // inv_path_trace.cu:144-145
-            weight = (float)((double)weight * (((1.0 / (double)kInvPiF) / (double)kPRR) / 1.0));
-            dst = tri;
-          } else {
-            if (m.flags & MAT_HAS_KS) speci = phong(m.shininess, nh, din, nd);
+          nd = unit(mk(fmaf(g.R[0][2], h.z, fmaf(g.R[0][1], h.y, g.R[0][0] * h.x)),
+                       fmaf(g.R[1][2], h.z, fmaf(g.R[1][1], h.y, g.R[1][0] * h.x)),
+                       fmaf(g.R[2][2], h.z, fmaf(g.R[2][1], h.y, g.R[2][0] * h.x))));
+          if (MODE != MODE_GRAPH) {
+            if (SPEC && (m.flags & MAT_HAS_KS)) speci = phong(m.shininess, nh, din, nd);
             coeff = (dot3(nd, nh) / psamp) / kPRR;
-            const float *kdt = kd + 3 * tri;
-            M = mk((M.x * (kdt[0] / kPiF + m.ks[0] * speci)) * coeff,
-                   (M.y * (kdt[1] / kPiF + m.ks[1] * speci)) * coeff,
-                   (M.z * (kdt[2] / kPiF + m.ks[2] * speci)) * coeff);
           }
-          d = nd;
           cont = true;
         }
       }
+    }
+
+    // ================= phase 2: next-event shadow ray (path_trace.cu:73-88)
+    V3 lo = mk(0.f, 0.f, 0.f);
+    if (__ballot(shadow)) {
+      float ts = 0.f;
+      int hs = -1;
+      if (shadow) hs = closest_hit(isect, nT, p, sd, ts);
+      const int et = shadow ? emit_tri[emitter] : -1;
+      if (shadow && hs == et) {  // must hit the sampled emitter itself
+        const V3 ne = shading_normal(geom[et], along(p, sd, ts));
+        const float ctp = -dot3(ne, sd);
+        if (!(ctp < 0.f)) {
+          const double td = (double)ts;
+          const TriMat &me = mat[et];
+          if (MODE == MODE_GRAPH) {
+            const float w2 = (float)(((double)((weight * ct) * ctp) / (td * td)) / (double)emit_pmf[emitter]);
+            double *e = acc + ((size_t)tri * nT + et) * kEdgeW;
+            const float wf = w2 * kInvPiF;  // BSDF(direct) factor 1/pi, inv_path_trace.cu:8
+            atomicAdd(e + 0, (double)w2);
+            atomicAdd(e + 1, (double)wf);
+            atomicAdd(e + 2, (double)(wf * pix.x));
+            atomicAdd(e + 3, (double)(wf * pix.y));
+            atomicAdd(e + 4, (double)(wf * pix.z));
+            atomicAdd(e + 5, (double)(wf * me.ke[0]));
+            atomicAdd(e + 6, (double)(wf * me.ke[1]));
+            atomicAdd(e + 7, (double)(wf * me.ke[2]));
+          } else {
+            const float s = (float)(((double)(ct * ctp) / (td * td)) / (double)emit_pmf[emitter]);
+            lo = mk(me.ke[0] * s, me.ke[1] * s, me.ke[2] * s);
+            const TriMat &m = mat[tri];
+            if (SPEC && (m.flags & MAT_HAS_KS)) specd = phong(m.shininess, nh, din, sd);
+            const float *kdt = kd + 3 * tri;
+            Ld = mk((kdt[0] + m.ks[0] * specd) * lo.x, (kdt[1] + m.ks[1] * specd) * lo.y,
+                    (kdt[2] + m.ks[2] * specd) * lo.z);
+          }
+        }
+      }
+    }
+
+    // ================= finalise the vertex
+    if (vertex) {
       if (MODE == MODE_ADJ) {  // vertex record k (layout [field][vertex][lane])
         float *rec = lds_rec + (size_t)k * kBlock + tid;
         const size_t fs = (size_t)vmax * kBlock;
@@ -302,15 +296,24 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(
         rec[5 * fs] = coeff;
         rec[6 * fs] = speci;
       }
-      if (MODE != MODE_GRAPH) {
-        L = mk(fmaf(Mp.x, Le.x + Ld.x, L.x), fmaf(Mp.y, Le.y + Ld.y, L.y), fmaf(Mp.z, Le.z + Ld.z, L.z));
-      }
-      if (cont) {
-        ++k;
+      if (MODE == MODE_GRAPH) {
+        if (cont) {
+          weight *= dot3(nd, nh);  // inv_path_trace.cu:144-145
+          weight = (float)((double)weight * (((1.0 / (double)kInvPiF) / (double)kPRR) / 1.0));
+          dst = tri;
+        }
       } else {
-        finished = true;
-        ++k;  // vertices recorded = k
+        L = mk(fmaf(M.x, Le.x + Ld.x, L.x), fmaf(M.y, Le.y + Ld.y, L.y), fmaf(M.z, Le.z + Ld.z, L.z));
+        if (cont) {
+          const TriMat &m = mat[tri];
+          const float *kdt = kd + 3 * tri;
+          M = mk((M.x * (kdt[0] / kPiF + m.ks[0] * speci)) * coeff, (M.y * (kdt[1] / kPiF + m.ks[1] * speci)) * coeff,
+                 (M.z * (kdt[2] / kPiF + m.ks[2] * speci)) * coeff);
+        }
       }
+      ++k;  // vertices so far
+      if (cont) d = nd;
+      else finished = true;
     }
 
     if (finished) {
@@ -333,11 +336,11 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(
           if (escaped) {
             const float *r = lds_rec + (size_t)(K - 1) * kBlock + tid;
             const int tk = __float_as_int(r[0]);
-            const float sd = r[4 * fs];
+            const float sdk = r[4 * fs];
             const TriMat &m = mat[tk];
             const float *kdt = kd + 3 * tk;
-            S = mk(Le.x + (kdt[0] + m.ks[0] * sd) * r[fs], Le.y + (kdt[1] + m.ks[1] * sd) * r[2 * fs],
-                   Le.z + (kdt[2] + m.ks[2] * sd) * r[3 * fs]);
+            S = mk(Le.x + (kdt[0] + m.ks[0] * sdk) * r[fs], Le.y + (kdt[1] + m.ks[1] * sdk) * r[2 * fs],
+                   Le.z + (kdt[2] + m.ks[2] * sdk) * r[3 * fs]);
           }
           for (int kk = K - 1; kk >= 0; --kk) {
             // prefix throughput M_kk (recomputed exactly as the forward did)
@@ -354,7 +357,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(
             const float *r = lds_rec + (size_t)kk * kBlock + tid;
             const int tk = __float_as_int(r[0]);
             const V3 lk = mk(r[fs], r[2 * fs], r[3 * fs]);
-            const float sd = r[4 * fs], ck = r[5 * fs], si = r[6 * fs];
+            const float sdk = r[4 * fs], ck = r[5 * fs], si = r[6 * fs];
             const bool last_esc = escaped && kk == K - 1;
             const bool continued = (kk < K - 1) || escaped;
             V3 dLd = Mk;
@@ -369,9 +372,9 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(
             atomicAdd(&lds_acc[tk * 3 + 2], (double)(az * gk.z));
             const TriMat &m = mat[tk];
             const float *kdt = kd + 3 * tk;
-            S = mk((Le.x + (kdt[0] + m.ks[0] * sd) * lk.x) + ((kdt[0] / kPiF + m.ks[0] * si) * ck) * S.x,
-                   (Le.y + (kdt[1] + m.ks[1] * sd) * lk.y) + ((kdt[1] / kPiF + m.ks[1] * si) * ck) * S.y,
-                   (Le.z + (kdt[2] + m.ks[2] * sd) * lk.z) + ((kdt[2] / kPiF + m.ks[2] * si) * ck) * S.z);
+            S = mk((Le.x + (kdt[0] + m.ks[0] * sdk) * lk.x) + ((kdt[0] / kPiF + m.ks[0] * si) * ck) * S.x,
+                   (Le.y + (kdt[1] + m.ks[1] * sdk) * lk.y) + ((kdt[1] / kPiF + m.ks[1] * si) * ck) * S.y,
+                   (Le.z + (kdt[2] + m.ks[2] * sdk) * lk.z) + ((kdt[2] / kPiF + m.ks[2] * si) * ck) * S.z);
           }
         }
       }
@@ -427,8 +430,9 @@ struct GpuScene {
   float *emit_cdf = nullptr, *emit_pmf = nullptr;
   float *ws = nullptr;  // per-sample radiance workspace
   size_t ws_bytes = 0;
-  int grid[3] = {0, 0, 0};  // resident workgroups per mode (0 = not queried)
-  size_t grid_lds[3] = {0, 0, 0};
+  bool has_ks = false;      // some material has a Phong lobe
+  int grid[6] = {0, 0, 0, 0, 0, 0};  // resident workgroups per (mode, spec) (0 = not queried)
+  size_t grid_lds[6] = {0, 0, 0, 0, 0, 0};
 };
 
 const HostScene &gpu_host(const GpuScene *s) { return s->host; }
@@ -457,6 +461,7 @@ GpuScene *gpu_upload(const HostScene &host, std::string *err) {
     gpu_free(s);
     return nullptr;
   }
+  for (const TriMat &m : host.mat) s->has_ks |= (m.flags & MAT_HAS_KS) != 0;
   s->on_device = true;
   return s;
 }
@@ -519,20 +524,21 @@ static int check_params(const GpuScene *s, const RenderParams &p) {
   return 0;
 }
 
-template <int MODE>
+template <int MODE, bool SPEC>
 static int resident_grid(GpuScene *s, size_t lds_bytes, int *grid) {
-  if (s->grid[MODE] == 0 || s->grid_lds[MODE] != lds_bytes) {
+  const int slot = MODE * 2 + (SPEC ? 1 : 0);
+  if (s->grid[slot] == 0 || s->grid_lds[slot] != lds_bytes) {
     int per_cu = 0, cus = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<MODE>, kBlock, lds_bytes));
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<MODE, SPEC>, kBlock, lds_bytes));
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device));
     if (per_cu <= 0) {
       gpu_set_error("trace kernel cannot be resident (LDS request too large?)");
       return -1;
     }
-    s->grid[MODE] = per_cu * cus;
-    s->grid_lds[MODE] = lds_bytes;
+    s->grid[slot] = per_cu * cus;
+    s->grid_lds[slot] = lds_bytes;
   }
-  *grid = s->grid[MODE];
+  *grid = s->grid[slot];
   return 0;
 }
 
@@ -552,17 +558,27 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   return a;
 }
 
-template <int MODE>
-static int launch(GpuScene *s, const TraceArgs &a, size_t lds, const float *kd_dev, float *out, const float *adj,
-                  double *grad, const uint8_t *target, double *edges, hipStream_t st) {
+template <int MODE, bool SPEC>
+static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float *kd_dev, float *out, const float *adj,
+                       double *grad, const uint8_t *target, double *edges, hipStream_t st) {
   int grid = 0;
-  if (resident_grid<MODE>(s, lds, &grid)) return -1;
+  if (resident_grid<MODE, SPEC>(s, lds, &grid)) return -1;
   if (a.n_samples == 0) return 0;
-  hipLaunchKernelGGL(trace_kernel<MODE>, dim3(grid), dim3(kBlock), lds, st, s->isect, s->geom, s->mat,
+  hipLaunchKernelGGL((trace_kernel<MODE, SPEC>), dim3(grid), dim3(kBlock), lds, st, s->isect, s->geom, s->mat,
                      kd_dev ? kd_dev : s->kd, s->emit_tri, s->emit_cdf, s->emit_pmf, a, out, adj, grad, target,
                      edges);
   HIP_TRY(hipGetLastError());
   return 0;
+}
+
+// The Phong paths (double-precision pow) are compiled only into the SPEC
+// instance, used when some material has Ks != 0; the shipped scenes have
+// none, and dropping the code lowers register pressure (occupancy).
+template <int MODE>
+static int launch(GpuScene *s, const TraceArgs &a, size_t lds, const float *kd_dev, float *out, const float *adj,
+                  double *grad, const uint8_t *target, double *edges, hipStream_t st) {
+  if (s->has_ks) return launch_inst<MODE, true>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
+  return launch_inst<MODE, false>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
 }
 
 int gpu_render_samples(GpuScene *s, const RenderParams &p, const float *kd_dev, float *samples_dev, void *stream) {

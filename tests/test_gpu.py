@@ -1,0 +1,272 @@
+"""GPU parity tests (run with -m gpu on an MI355X).
+
+Every compute call goes through the C ABI of lib/libipt_amd.so.  Bars:
+  * forward per-sample radiance and per-pixel HDR: BIT-IDENTICAL to the CPU
+    oracle on the same seeds (canonical arithmetic);
+  * adjoint gradient and graph bins: fp64 sums whose order differs (atomics),
+    so rtol 1e-9 against the oracle; the compressed createGraph floats are
+    compared at rtol 1e-6;
+  * at the BASELINE.json sizes (oracle too slow): size-independent properties
+    -- row-band sharding reproduces the full frame bit-for-bit, the adjoint is
+    linear in the adjoint image and matches central finite differences of the
+    GPU forward, and the reference's golden render statistics hold.
+"""
+import ctypes as C
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import CORNELL, CUBE_OBJ, SCENE0, SPHERE_OBJ, TESTS, product_scene
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    torch.cuda.set_device(0)
+    from inverse_path_tracer_amd import _native
+
+    assert _native.device_count() >= 1
+    yield
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+@pytest.fixture(scope="module")
+def scenes(oracle):
+    return {
+        "cornell": (product_scene(CORNELL), oracle.OracleScene(CORNELL)),
+        "scene0": (product_scene(SCENE0), oracle.OracleScene(SCENE0)),
+    }
+
+
+# ------------------------------------------------------------- forward
+@pytest.mark.parametrize("name,W,H,spp,mb,seed", [
+    ("cornell", 128, 128, 8, 2, 0),          # BASELINE config C1 (the CPU plumbing config)
+    ("cornell", 64, 48, 16, 4, 1),
+    ("scene0", 64, 64, 16, None, 7),         # reference semantics: unbounded
+    ("scene0", 40, 30, 8, 0, 3),             # direct lighting only
+    ("scene0", 33, 17, 5, 8, 2**33 + 5),     # odd sizes, 64-bit seed
+    ("scene0", 1, 1, 1, 4, 0),               # single sample
+])
+def test_forward_samples_bit_exact(scenes, name, W, H, spp, mb, seed):
+    P, Q = scenes[name]
+    got = P.render_samples(W, H, spp, mb, seed)
+    want, _ = Q.render_samples(W, H, spp, mb, seed)
+    assert np.array_equal(bits(got), bits(want))
+
+
+def test_forward_hdr_and_tonemap_bit_exact(scenes, oracle):
+    P, Q = scenes["scene0"]
+    hdr, u8 = P.render(48, 40, 12, 4, 5, ldr=True)
+    s, _ = Q.render_samples(48, 40, 12, 4, 5)
+    hq, uq = oracle.pixel_mean(s, 48 * 40, 12)
+    assert np.array_equal(bits(hdr.reshape(-1, 3)), bits(hq))
+    assert np.array_equal(u8.reshape(-1, 3), uq)
+
+
+def test_sphere_scene_bit_exact(oracle):
+    recs = CORNELL + [((0.3, -1.2, 4.2), (0.0, 0.4, 0.0), (1.2, 1.2, 1.2), SPHERE_OBJ, "*Kd 0.2 0.6 0.3*")]
+    P, Q = product_scene(recs), oracle.OracleScene(recs)
+    assert P.nT == 18 + 1280
+    got = P.render_samples(24, 24, 4, 3, 9)
+    want, _ = Q.render_samples(24, 24, 4, 3, 9)
+    assert np.array_equal(bits(got), bits(want))
+
+
+def test_specular_material_bit_exact(oracle, tmp_path):
+    mtl = tmp_path / "s.mtl"
+    mtl.write_text("newmtl shiny\nKd 0.3 0.3 0.3\nKs 0.5 0.4 0.3\nNs 20\n")
+    obj = tmp_path / "s.obj"
+    obj.write_text(open(CUBE_OBJ).read().replace("f 1 2 3", "mtllib s.mtl\nusemtl shiny\nf 1 2 3", 1))
+    recs = CORNELL + [((0, -1.5, 4), (0, 0.3, 0), (1, 1, 1), str(obj), str(mtl))]
+    P, Q = product_scene(recs), oracle.OracleScene(recs)
+    assert np.any(P.triangles()[:, 28:31] > 0)
+    got = P.render_samples(32, 32, 8, 4, 4)
+    want, _ = Q.render_samples(32, 32, 8, 4, 4)
+    assert np.array_equal(bits(got), bits(want))
+    adj = np.random.RandomState(0).uniform(-1, 1, (32, 32, 3)).astype(np.float32)
+    np.testing.assert_allclose(P.adjoint(adj, 32, 32, 8, 4, 4), Q.adjoint(32, 32, 8, 4, 4, adj), rtol=1e-9, atol=1e-12)
+
+
+def test_no_emitters_is_black_not_nan(oracle):
+    recs = [((0, -1.5, 4), (0, 0, 0), (1, 1, 1), CUBE_OBJ, "*Kd 0.5 0.5 0.5*")]
+    P, Q = product_scene(recs), oracle.OracleScene(recs)
+    assert P.nE == 0
+    got = P.render_samples(16, 16, 4, None, 0)
+    want, _ = Q.render_samples(16, 16, 4, None, 0)
+    assert np.array_equal(bits(got), bits(want)) and np.all(got == 0)
+
+
+def test_empty_band_and_bad_params(scenes):
+    from inverse_path_tracer_amd import NativeError
+
+    P, _ = scenes["scene0"]
+    assert P.render(16, 16, 2, 2, 0, row_begin=5, row_end=5).shape == (0, 16, 3)
+    with pytest.raises(NativeError):
+        P.render(16, 16, 0, 2, 0)
+    with pytest.raises(NativeError):
+        P.render(16, 16, 2, 2, 0, row_begin=3, row_end=20)
+    with pytest.raises(NativeError, match="max_bounces"):
+        P.adjoint(np.zeros((8, 8, 3), np.float32), 8, 8, 1, None, 0)
+
+
+# ------------------------------------------------------------- sharding (C2/C4 sizes)
+@pytest.mark.parametrize("W,H,spp,mb,world", [(512, 512, 64, 4, 8), (1024, 1024, 32, 8, 8), (512, 512, 64, 4, 3)])
+def test_row_band_sharding_bit_exact(scenes, W, H, spp, mb, world):
+    from inverse_path_tracer_amd.distributed import shard_rows
+
+    P, _ = scenes["scene0"]
+    full = P.render(W, H, spp, mb, 0)
+    bands = [P.render(W, H, spp, mb, 0, *shard_rows(H, world, r)) for r in range(world)]
+    assert np.array_equal(bits(np.concatenate(bands)), bits(full))
+
+
+# ------------------------------------------------------------- adjoint
+@pytest.mark.parametrize("name,W,H,spp,mb,seed", [
+    ("scene0", 64, 64, 8, 4, 3), ("scene0", 31, 23, 4, 8, 1), ("cornell", 48, 48, 8, 2, 6), ("scene0", 16, 16, 4, 0, 2)])
+def test_adjoint_matches_oracle(scenes, name, W, H, spp, mb, seed):
+    P, Q = scenes[name]
+    adj = np.random.RandomState(seed).uniform(-1, 1, (H, W, 3)).astype(np.float32)
+    g = P.adjoint(adj, W, H, spp, mb, seed)
+    want = Q.adjoint(W, H, spp, mb, seed, adj)
+    np.testing.assert_allclose(g, want, rtol=1e-9, atol=1e-12)
+
+
+def test_adjoint_row_bands_sum_to_full(scenes):
+    from inverse_path_tracer_amd.distributed import shard_rows
+
+    P, _ = scenes["scene0"]
+    adj = np.random.RandomState(4).uniform(-1, 1, (128, 128, 3)).astype(np.float32)
+    full = P.adjoint(adj, 128, 128, 16, 4, 0)
+    parts = sum(P.adjoint(adj, 128, 128, 16, 4, 0, *shard_rows(128, 4, r)) for r in range(4))
+    np.testing.assert_allclose(parts, full, rtol=1e-10)
+
+
+def _loss(P, kd, adj, W, H, spp, mb, seed):
+    P.materials = kd
+    return float((adj.astype(np.float64) * P.render(W, H, spp, mb, seed).astype(np.float64)).sum())
+
+
+def test_adjoint_fd_at_c3_size(scenes):
+    """BASELINE config C3 (scenes/0.txt, 512x512x64, 4 bounces): gradient vs
+    central differences of the GPU forward under common random numbers."""
+    P, _ = scenes["scene0"]
+    W = H = 512
+    spp, mb, seed = 64, 4, 0
+    kd0 = P.materials
+    adj = np.ones((H, W, 3), np.float32)
+    g = P.adjoint(adj, W, H, spp, mb, seed)
+    h = 1e-2
+    for t, c in [(0, 0), (8, 1), (12, 2), (14, 0), (19, 1), (25, 0)]:
+        kp, km = kd0.copy(), kd0.copy()
+        kp[t, c] += h
+        km[t, c] -= h
+        fd = (_loss(P, kp, adj, W, H, spp, mb, seed) - _loss(P, km, adj, W, H, spp, mb, seed)) / (2 * h)
+        assert abs(fd - g[t, c]) <= 1e-3 * abs(g[t, c]) + 1e-2, (t, c, fd, g[t, c])
+    P.materials = kd0
+
+
+def test_adjoint_linear_in_adjoint_image(scenes):
+    P, _ = scenes["scene0"]
+    a1 = np.random.RandomState(1).uniform(-1, 1, (256, 256, 3)).astype(np.float32)
+    a2 = np.random.RandomState(2).uniform(-1, 1, (256, 256, 3)).astype(np.float32)
+    g1 = P.adjoint(a1, 256, 256, 16, 4, 0)
+    g2 = P.adjoint(a2, 256, 256, 16, 4, 0)
+    g12 = P.adjoint(a1 + a2, 256, 256, 16, 4, 0)
+    np.testing.assert_allclose(g12, g1 + g2, rtol=1e-4, atol=1e-6 * np.abs(g1).max())
+
+
+def test_torch_autograd_op(scenes, oracle):
+    from inverse_path_tracer_amd import torch_ops
+
+    P, Q = scenes["scene0"]
+    kd = torch.tensor(P.materials, device="cuda", requires_grad=True)
+    img = torch_ops.render(P, kd, 40, 40, 8, 4, 12)
+    s, _ = Q.render_samples(40, 40, 8, 4, 12)
+    hq, _ = oracle.pixel_mean(s, 1600, 8)
+    assert np.array_equal(bits(img.detach().cpu().numpy().reshape(-1, 3)), bits(hq))
+    adj = torch.rand((40, 40, 3), device="cuda") - 0.5
+    (img * adj).sum().backward()
+    np.testing.assert_allclose(kd.grad.double().cpu().numpy(), Q.adjoint(40, 40, 8, 4, 12, adj.cpu().numpy()),
+                               rtol=1e-5, atol=1e-9)
+    # band render through autograd
+    kd2 = torch.tensor(P.materials, device="cuda", requires_grad=True)
+    band = torch_ops.render(P, kd2, 40, 40, 8, 4, 12, 10, 25)
+    (band * adj[10:25]).sum().backward()
+    want = Q.adjoint(40, 40, 8, 4, 12, adj.cpu().numpy(), 10, 25)
+    np.testing.assert_allclose(kd2.grad.double().cpu().numpy(), want, rtol=1e-5, atol=1e-9)
+
+
+# ------------------------------------------------------------- graph
+@pytest.mark.parametrize("W,H,spp,mb,seed", [(64, 64, 8, None, 5), (50, 40, 4, 3, 1)])
+def test_graph_matches_oracle(scenes, W, H, spp, mb, seed):
+    P, Q = scenes["scene0"]
+    tgt = np.random.RandomState(seed).randint(0, 256, (H, W, 3)).astype(np.uint8)
+    acc, data = P.graph(tgt, W, H, spp, mb, seed)
+    acc_q, data_q = Q.graph(W, H, spp, mb, seed, tgt)
+    np.testing.assert_allclose(acc, acc_q, rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(data, data_q, rtol=1e-6, atol=1e-7)
+
+
+# ------------------------------------------------------------- legacy drop-in
+def test_legacy_ipt_cuda_pipeline(oracle, tmp_path, monkeypatch):
+    """generate_data / render_with_materials through the reference's module
+    surface, at a small legacy configuration."""
+    from inverse_path_tracer_amd import _native as N
+    from inverse_path_tracer_amd import ipt_cuda as M
+    from inverse_path_tracer_amd import png_read, png_write
+
+    assets = os.path.join(os.path.dirname(TESTS), "assets")
+    monkeypatch.chdir(assets)  # scene files hold CWD-relative paths, like the reference
+    N.lib().ipt_legacy_config(64, 64, 8, -1, 77)
+    try:
+        tgt = np.random.RandomState(3).randint(0, 256, (64, 64, 3)).astype(np.uint8)
+        tpath = str(tmp_path / "t.png")
+        png_write(tpath, tgt)
+        w, pixel, light, labels = M.generate_data("scenes/0.txt", tpath)
+        Q = oracle.OracleScene(SCENE0)
+        _, data_q = Q.graph(64, 64, 8, None, 77, tgt)
+        size = 31 * 30
+        np.testing.assert_allclose(w, data_q[:size].reshape(31, 30), rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(pixel, data_q[size:4 * size].reshape(31, 30, 3), rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(labels, Q.get_materials())
+        kd = np.random.RandomState(4).uniform(0, 1, (30, 3)).astype(np.float32)
+        out = str(tmp_path / "r.png")
+        M.render_with_materials("scenes/0.txt", out, torch.from_numpy(kd))
+        Q.set_materials(kd)
+        _, u8, _ = Q.render(64, 64, 8, None, 77)
+        assert np.array_equal(png_read(out), u8)
+        with pytest.raises(N.NativeError, match="expected 64x64"):
+            small = str(tmp_path / "small.png")
+            png_write(small, tgt[:32])
+            M.generate_data("scenes/0.txt", small)
+    finally:
+        N.lib().ipt_legacy_config(500, 500, 100, -1, -1)
+
+
+def test_statistical_kat_full_reference_config(scenes):
+    """The reference's own configuration (500x500, 100 spp, unbounded) vs
+    preds/0_true.png: region means within 1 level, mean |diff| at the MC-noise
+    level of two independent reference renders (3.5)."""
+    from inverse_path_tracer_amd import png_read
+
+    P, _ = scenes["scene0"]
+    _, u8 = P.render(500, 500, 100, None, 31337, ldr=True)
+    g = json.load(open(os.path.join(TESTS, "golden", "preds_0_true_stats.json")))
+    from test_oracle import region_means
+
+    for k, v in region_means(u8, 1.0).items():
+        assert np.abs(v - np.array(g["regions"][k])).max() < (1.0 if k != "cube_front" else 1.5), k
+    ref = png_read(os.path.join(TESTS, "golden", "preds_0_true.png")).astype(np.float64)
+    noise = np.abs(u8.astype(np.float64) - ref).mean()
+    assert abs(noise - g["noise_mean_abs_true_vs_pred"]) < 0.3
+    blocks = u8.astype(np.float64).reshape(50, 10, 50, 10, 3).mean(axis=(1, 3))
+    assert np.abs(blocks - np.array(g["block10_means"])).mean() < 0.6

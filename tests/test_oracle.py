@@ -1,0 +1,226 @@
+"""The CPU oracle, pinned against the reference's own fixtures.
+
+The reference cannot run here, so the oracle is pinned by: the golden render
+preds/0_true.png (region statistics, committed in tests/golden), temp.pt's
+triangle ordering, the reference's compile-time constants, and internal
+properties (finite differences, bounce monotonicity).  cuRAND XORWOW has no
+reference vector: it is checked against an independent numpy restatement of
+the published algorithm ("parity unpinned" for the RNG bits themselves).
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from conftest import CORNELL, SCENE0, TESTS
+
+GOLDEN = os.path.join(TESTS, "golden")
+
+
+# ----------------------------------------------------------------- RNG
+def _curand_uniform_stream(seed, n):
+    """Independent numpy restatement of curand_init(seed,0,0)+curand_uniform."""
+    M = 0xFFFFFFFF
+    s0 = (seed & M) ^ 0xAAD26B49
+    s1 = ((seed >> 32) & M) ^ 0xF7DCEFDD
+    t0 = (1099087573 * s0) & M
+    t1 = (2591861531 * s1) & M
+    d = (6615241 + t1 + t0) & M
+    v = [(123456789 + t0) & M, 362436069 ^ t0, (521288629 + t1) & M, 88675123 ^ t1, (5783321 + t0) & M]
+    out = []
+    for _ in range(n):
+        t = v[0] ^ (v[0] >> 2)
+        v = v[1:] + [((v[4] ^ ((v[4] << 4) & M)) ^ (t ^ ((t << 1) & M))) & M]
+        d = (d + 362437) & M
+        x = (v[4] + d) & M
+        out.append(np.float32(np.float32(x) * np.float32(2.3283064e-10) + np.float32(1.1641532e-10)))
+    return out
+
+
+@pytest.mark.parametrize("seed", [0, 1, 12345, 2**32 + 7, 0xDEADBEEFCAFE])
+def test_xorwow_matches_restatement(oracle, seed):
+    want = _curand_uniform_stream(seed, 12)
+    got = [oracle.lib().oro_uniform_at(seed, k) for k in range(12)]
+    assert [np.float32(g) for g in got] == want
+    assert all(0.0 < g <= 1.0 for g in got)
+
+
+def test_uniform_constants_are_powers_of_two():
+    assert float(np.float32(2.3283064e-10)) == 2.0 ** -32
+    assert float(np.float32(1.1641532e-10)) == 2.0 ** -33
+
+
+# ----------------------------------------------------------------- math
+def test_sincos_correctly_rounded(oracle):
+    import ctypes as C
+
+    xs = np.random.RandomState(0).uniform(0, 2 * np.pi, 20000).astype(np.float32)
+    s, c = C.c_float(), C.c_float()
+    bad = 0
+    for x in xs:
+        oracle.lib().oro_sincos(float(x), C.byref(s), C.byref(c))
+        bad += (np.float32(s.value) != np.float32(math.sin(float(x)))) + (np.float32(c.value) != np.float32(math.cos(float(x))))
+    assert bad <= 2  # correctly rounded up to astronomically rare halfway cases
+
+
+def test_log_exp_pow(oracle):
+    L = oracle.lib()
+    for x in np.random.RandomState(1).uniform(1e-12, 1e6, 2000):
+        assert abs(L.oro_log(x) - math.log(x)) <= 4e-16 * max(1.0, abs(math.log(x)))
+    for x in np.random.RandomState(2).uniform(-700, 700, 2000):
+        assert abs(L.oro_exp(x) - math.exp(x)) <= 4e-16 * math.exp(x)
+    assert L.oro_powf(2.0, 10.0) == 1024.0
+    assert L.oro_powf(-2.0, 3.0) == -8.0
+    assert L.oro_powf(-2.0, 2.0) == 4.0
+    assert math.isnan(L.oro_powf(-2.0, 0.5))
+    assert L.oro_powf(0.0, 3.0) == 0.0 and L.oro_powf(5.0, 0.0) == 1.0
+
+
+# ----------------------------------------------------------------- scene
+def test_scene0_counts_and_camera(oracle):
+    cb = oracle.OracleScene(CORNELL)
+    s0 = oracle.OracleScene(SCENE0)
+    assert (cb.nT, cb.nE) == (18, 2)
+    assert (s0.nT, s0.nE) == (30, 2)
+    cam = s0.camera()  # scene.h:49-77 default camera = diag(-1, 1, 1, 1)
+    assert np.array_equal(np.abs(cam), np.diag([1.0, 1.0, 1.0, 1.0]).astype(np.float32))
+    assert cam[0, 0] == -1.0
+    tri = s0.triangles()
+    assert set(np.nonzero(tri[:, 56] >= 0)[0].tolist()) == {16, 17}  # emitters
+    assert np.allclose(tri[16:18, 31:34], 10.0)
+
+
+def test_material_order_matches_temp_pt(oracle):
+    """temp.pt (reference fixture) is a per-triangle Kd prediction for a
+    30-triangle scenes/*.txt scene; its colour pattern pins triangle order."""
+    kd = oracle.OracleScene(SCENE0).get_materials()
+    pred = np.load(os.path.join(GOLDEN, "temp_pt_materials.npy"))
+    assert pred.shape == kd.shape == (30, 3)
+    assert np.argmin(kd[12]) == np.argmin(pred[12]) == 0  # cyan right wall: red lowest
+    assert np.argmin(kd[13]) == np.argmin(pred[13]) == 0
+    for r in (14, 15):  # orange left wall: red highest, blue lowest
+        assert np.argmax(kd[r]) == np.argmax(pred[r]) == 0
+        assert np.argmin(kd[r]) == np.argmin(pred[r]) == 2
+    for r in range(18, 30):  # cube, scenes/0.txt Kd (0.90, 0.59, 0.007): blue lowest
+        assert np.argmin(kd[r]) == 2
+    assert np.mean([np.argmin(pred[r]) == 2 for r in range(18, 30)]) > 0.5
+    assert np.abs(kd - pred).mean() < 0.25
+
+
+# ----------------------------------------------------------------- KAT
+REGIONS = {"global": [0, 500, 0, 500], "light": [95, 135, 200, 300], "back_wall": [200, 280, 200, 300],
+           "floor": [420, 480, 150, 350], "cube_top": [310, 318, 225, 275], "cube_front": [340, 380, 225, 275],
+           "cyan_wall_left": [150, 350, 20, 120], "orange_wall_right": [150, 350, 380, 480],
+           "ceiling": [20, 60, 150, 350]}
+
+
+def region_means(u8, scale):
+    out = {}
+    for k, (r0, r1, c0, c1) in REGIONS.items():
+        a, b = int(r0 * scale), max(int(r1 * scale), int(r0 * scale) + 1)
+        out[k] = u8[a:b, int(c0 * scale):int(c1 * scale)].reshape(-1, 3).astype(np.float64).mean(0)
+    return out
+
+
+def test_statistical_kat_vs_reference_render(oracle):
+    """scenes/0.txt at the reference's 100 spp, unbounded bounces, 125x125
+    (the per-pixel estimator -- hence the tonemap bias -- is the reference's);
+    every region of preds/0_true.png within 1.5 levels.  This pins the
+    reference's quirks: the light plateau (~241, stale-L_e re-add) and the
+    cube top's blue (~3, direct term without 1/pi)."""
+    g = json.load(open(os.path.join(GOLDEN, "preds_0_true_stats.json")))
+    sc = oracle.OracleScene(SCENE0)
+    _, u8, _ = sc.render(125, 125, 100, None, 3)
+    got = region_means(u8, 125 / 500)
+    for k, v in got.items():
+        tol = 1.0 if k == "global" else 1.5
+        assert np.abs(v - np.array(g["regions"][k])).max() < tol, (k, v, g["regions"][k])
+    assert 238 < got["light"].min() and got["light"].max() < 245
+
+
+def test_max_bounces_monotone_prefix(oracle):
+    """max_bounces=B stops a path after its (B+1)-th vertex: sample values are
+    prefixes of the unbounded estimator (all terms >= 0)."""
+    sc = oracle.OracleScene(SCENE0)
+    vals = [sc.render_samples(24, 24, 4, b, 11)[0] for b in (0, 1, 2, 4, None)]
+    for lo, hi in zip(vals, vals[1:]):
+        assert np.all(lo <= hi)
+    _, casts0 = sc.render_samples(24, 24, 4, 0, 11)
+    assert casts0 <= 2 * 24 * 24 * 4  # camera ray + at most one shadow ray
+
+
+# ----------------------------------------------------------------- adjoint
+def test_adjoint_matches_central_differences(oracle):
+    """The path-replay adjoint equals d(sum adj*I)/dKd of the float forward
+    estimator under common random numbers (central FD; the estimator is a
+    polynomial in Kd for fixed draws)."""
+    W = H = 20
+    spp, mb, seed = 4, 3, 5
+    sc = oracle.OracleScene(SCENE0)
+    adj = np.random.RandomState(3).uniform(-1, 1, (H, W, 3)).astype(np.float32)
+    g = sc.adjoint(W, H, spp, mb, seed, adj)
+    kd0 = sc.get_materials()
+
+    def loss(kd):
+        sc.set_materials(kd)
+        hdr, _, _ = sc.render(W, H, spp, mb, seed)
+        return float((adj.astype(np.float64) * hdr.astype(np.float64)).sum())
+
+    h = 1e-2
+    for (t, c) in [(0, 0), (4, 1), (10, 2), (12, 0), (14, 1), (20, 2), (27, 0)]:
+        kp, km = kd0.copy(), kd0.copy()
+        kp[t, c] += h
+        km[t, c] -= h
+        fd = (loss(kp) - loss(km)) / (2 * h)
+        assert abs(fd - g[t, c]) <= 2e-3 * max(1.0, abs(g[t, c])), (t, c, fd, g[t, c])
+    sc.set_materials(kd0)
+    assert np.all(g[16:18] == g[16:18])  # finite everywhere
+
+
+# ----------------------------------------------------------------- graph
+def _compress_np(nT, acc):
+    """numpy restatement of DataWrapper::compress (inv_scene.h:87-115)."""
+    acc = acc.reshape(nT + 1, nT, 8)
+    w = np.log(acc[..., 0].astype(np.float32) + np.float32(1)).astype(np.float32)
+    fs = acc[..., 1].astype(np.float32)
+    den = np.where(fs != 0, fs, np.float32(1)).astype(np.float32)
+    pix = (acc[..., 2:5].astype(np.float32) / den[..., None]).astype(np.float32)
+    lig = (acc[..., 5:8].astype(np.float32) / den[..., None]).astype(np.float32)
+    tot = np.zeros(nT + 1, np.float32)
+    for d in range(nT + 1):
+        t = np.float32(0)
+        for s in range(nT):
+            t = np.float32(t + w[d, s])
+        tot[d] = t
+    wt = np.where(tot[:, None] != 0, w / np.where(tot[:, None] != 0, tot[:, None], 1), 0).astype(np.float32)
+    return np.concatenate([wt.ravel(), pix.ravel(), lig.ravel()])
+
+
+def test_compress_restatement(oracle):
+    nT = 7
+    rs = np.random.RandomState(4)
+    acc = rs.uniform(0, 50, ((nT + 1) * nT, 8))
+    acc[3] = 0.0  # an empty edge
+    acc[5, 1] = 0.0  # zero factor sum -> divide by 1
+    want = _compress_np(nT, acc)
+    got = oracle.compress(nT, acc)
+    np.testing.assert_allclose(got, want, rtol=2e-6, atol=1e-7)
+
+
+def test_graph_structure(oracle):
+    sc = oracle.OracleScene(SCENE0)
+    tgt = np.full((16, 16, 3), 128, np.uint8)
+    acc, data = sc.graph(16, 16, 4, None, 1, tgt)
+    nT = sc.nT
+    acc = acc.reshape(nT + 1, nT, 8)
+    assert acc[nT, :, 0].sum() > 0  # eye edges exist
+    # every eye-edge update carries the target pixel (128/255) times w*f
+    m = acc[nT, :, 1] > 0
+    np.testing.assert_allclose(acc[nT, m, 2] / acc[nT, m, 1], 128 / 255, rtol=1e-5)
+    # light edges: only emitters (16, 17) are sources of direct-lighting light
+    assert np.all(acc[:, :16, 5:8] == 0) and np.all(acc[:, 18:, 5:8] == 0)
+    w = data[: (nT + 1) * nT].reshape(nT + 1, nT)
+    rows = w.sum(1)
+    assert np.all((np.abs(rows - 1) < 1e-5) | (rows == 0))  # row-normalised log weights

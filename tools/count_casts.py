@@ -1,0 +1,30 @@
+"""Counts C-bar = ray casts per sample (camera/continuation + shadow) with the
+CPU oracle over the FULL benchmark configurations.  The
+printed constants are committed in bench.py (CASTS_PER_SAMPLE)."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import oracle_lib as O  # noqa: E402
+from conftest import CORNELL, SCENE0  # noqa: E402
+
+CONFIGS = {
+    "C2_cornell_512x512x64_b4": (CORNELL, 512, 512, 64, 4, 0),
+    "C3_scene0_512x512x64_b4": (SCENE0, 512, 512, 64, 4, 0),
+}
+out = {}
+for name, (recs, W, H, spp, mb, seed) in CONFIGS.items():
+    sc = O.OracleScene(recs)
+    total, n, t0 = 0, 0, time.time()
+    step = 32  # rows per chunk (bounded memory)
+    for r in range(0, H, step):
+        s, c = sc.render_samples(W, H, spp, mb, seed, r * W * spp, min(H, r + step) * W * spp)
+        total += c
+        n += len(s)
+    out[name] = {"casts_per_sample": total / n, "samples": n, "nT": sc.nT, "seconds": round(time.time() - t0, 1)}
+    print(name, out[name], flush=True)
+with open(os.path.join(ROOT, "profiles", "casts_per_sample.json"), "w") as f:
+    json.dump(out, f, indent=1)

@@ -1,0 +1,93 @@
+"""A/B timing of kernel variants (lib/variants/libipt_*.so) in ONE process,
+interleaved rounds (cdna_hip_programming.md §5.4 rule 24).  Each variant is
+checked bit-exact against the default library on a small frame first."""
+import ctypes as C
+import glob
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from inverse_path_tracer_amd import _native as N  # noqa: E402
+
+A = os.path.join(ROOT, "assets")
+SCENES = {
+    "cornell": [(A + "/CornellBox/CornellBox-Empty-CO.obj", A + "/CornellBox/CornellBox-Empty-CO.mtl", (0, 0, 4), (0, 0, 0), (2, 2, 2))],
+}
+SCENES["scene0"] = SCENES["cornell"] + [(A + "/shapes/cube.obj", "*Kd 0.9041462985304743 0.5854651848798454 0.007022117649276849*",
+                                          (0, -1.5, 4), (0, 0, 0), (1, 1, 1))]
+
+
+def load(path):
+    L = C.CDLL(path, mode=os.RTLD_LOCAL)
+    for name, (res, args) in N.SIGNATURES.items():
+        f = getattr(L, name)
+        f.restype, f.argtypes = res, args
+    return L
+
+
+def scene(L, recs):
+    n = len(recs)
+    pos = np.array([r[2] for r in recs], np.float32)
+    ori = np.array([r[3] for r in recs], np.float32)
+    scl = np.array([r[4] for r in recs], np.float32)
+    objs = (C.c_char_p * n)(*[r[0].encode() for r in recs])
+    mtls = (C.c_char_p * n)(*[r[1].encode() for r in recs])
+    h = C.c_void_p(0)
+    assert L.ipt_load_scene(n, pos.ctypes.data_as(N.fp), ori.ctypes.data_as(N.fp), scl.ctypes.data_as(N.fp), objs,
+                            mtls, C.byref(h)) > 0
+    return h
+
+
+def main():
+    names = sys.argv[1:] or sorted(os.path.basename(p)[7:-3] for p in glob.glob(os.path.join(ROOT, "inverse_path_tracer_amd/lib/variants/libipt_*.so")))
+    libs = {n: load(os.path.join(ROOT, "inverse_path_tracer_amd/lib/variants/libipt_%s.so" % n)) for n in names}
+    ref = load(N.LIB_PATH)
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream().cuda_stream
+    out = {}
+    for sname, recs in SCENES.items():
+        hs = {n: scene(L, recs) for n, L in libs.items()}
+        href = scene(ref, recs)
+        # correctness: small frame bit-exact vs default library
+        p = N.make_params(64, 64, 8, 4, 123)
+        want = np.zeros((64 * 64 * 8, 3), np.float32)
+        assert ref.ipt_render_samples_host(href, C.byref(p), want.ctypes.data_as(N.fp)) == 0
+        for n, L in libs.items():
+            got = np.zeros_like(want)
+            assert L.ipt_render_samples_host(hs[n], C.byref(p), got.ctypes.data_as(N.fp)) == 0
+            print(sname, n, "bit-exact" if np.array_equal(got.view(np.uint32), want.view(np.uint32)) else "MISMATCH", flush=True)
+        p = N.make_params(512, 512, 64, 4, 0)
+        buf = torch.empty((512 * 512 * 64, 3), device=dev)
+        adj = torch.ones((512, 512, 3), device=dev)
+        g = torch.zeros((64, 3), dtype=torch.float64, device=dev)
+        times = {n: {"fwd": [], "adj": []} for n in libs}
+        for rnd in range(6):
+            for n, L in libs.items():
+                for kind in ("fwd", "adj"):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(3):
+                        if kind == "fwd":
+                            assert L.ipt_render_samples_dev(hs[n], C.byref(p), None, buf.data_ptr(), st) == 0
+                        else:
+                            assert L.ipt_adjoint_dev(hs[n], C.byref(p), None, adj.data_ptr(), g.data_ptr(), st) == 0
+                    e1.record()
+                    torch.cuda.synchronize()
+                    if rnd > 0:
+                        times[n][kind].append(e0.elapsed_time(e1) / 3)
+        for n in libs:
+            f, a = np.median(times[n]["fwd"]), np.median(times[n]["adj"])
+            out[sname + ":" + n] = {"fwd_ms": round(f, 4), "adj_ms": round(a, 4),
+                                    "fwd_Msps": round(512 * 512 * 64 / f / 1e3, 1), "adj_Msps": round(512 * 512 * 64 / a / 1e3, 1)}
+            print(sname, n, out[sname + ":" + n], flush=True)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
