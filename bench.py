@@ -113,10 +113,10 @@ def main():
         p = params(step)
         if ev is not None:
             ev[0].record(stream)
-        N.check(L.ipt_render_samples_dev(scene.handle, C.byref(p), None, samples.data_ptr(), st))
+        N.check(L.ipt_render_samples_sm_dev(scene.handle, C.byref(p), None, samples.data_ptr(), st))
         if ev is not None:
             ev[1].record(stream)
-        N.check(L.ipt_pixel_mean_dev(samples.data_ptr(), npix, SPP, hdr.data_ptr(), None, st))
+        N.check(L.ipt_pixel_mean_sm_dev(samples.data_ptr(), npix, SPP, hdr.data_ptr(), None, st))
 
     def bwd(step):
         p = params(step)

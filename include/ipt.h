@@ -113,6 +113,12 @@ int ipt_render_samples_dev(void *scene, const ipt_params_t *p, const float *kd_d
                            void *stream);
 int ipt_pixel_mean_dev(const float *samples_dev, int64_t npix, int spp, float *hdr_dev, uint8_t *ldr_dev,
                        void *stream);
+/* The same two steps over a sample-major buffer ([s][pixel][3], rows*W*spp*3
+ * floats): the layout ipt_render_dev uses internally (coalesced mean). */
+int ipt_render_samples_sm_dev(void *scene, const ipt_params_t *p, const float *kd_dev, float *samples_dev,
+                              void *stream);
+int ipt_pixel_mean_sm_dev(const float *samples_dev, int64_t npix, int spp, float *hdr_dev, uint8_t *ldr_dev,
+                          void *stream);
 int ipt_adjoint_dev(void *scene, const ipt_params_t *p, const float *kd_dev, const float *adj_dev, double *grad_dev,
                     void *stream);
 int ipt_graph_dev(void *scene, const ipt_params_t *p, const uint8_t *target_dev, double *acc_dev, void *stream);

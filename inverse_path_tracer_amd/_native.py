@@ -81,6 +81,8 @@ SIGNATURES = {
     "ipt_render_dev": (C.c_int, [vp, pp, vp, vp, vp, vp]),
     "ipt_render_samples_dev": (C.c_int, [vp, pp, vp, vp, vp]),
     "ipt_pixel_mean_dev": (C.c_int, [vp, C.c_int64, C.c_int, vp, vp, vp]),
+    "ipt_render_samples_sm_dev": (C.c_int, [vp, pp, vp, vp, vp]),
+    "ipt_pixel_mean_sm_dev": (C.c_int, [vp, C.c_int64, C.c_int, vp, vp, vp]),
     "ipt_adjoint_dev": (C.c_int, [vp, pp, vp, vp, vp, vp]),
     "ipt_graph_dev": (C.c_int, [vp, pp, vp, vp, vp]),
     "ipt_png_write": (C.c_int, [C.c_char_p, C.c_int, C.c_int, u8p]),

@@ -302,6 +302,22 @@ int ipt_pixel_mean_dev(const float *samples_dev, int64_t npix, int spp, float *h
   return gpu_status(ipt::gpu_pixel_mean(samples_dev, npix, spp, hdr_dev, ldr_dev, stream));
 }
 
+int ipt_render_samples_sm_dev(void *scene, const ipt_params_t *p, const float *kd_dev, float *samples_dev,
+                              void *stream) {
+  GpuScene *s = as_scene(scene);
+  if (!s || !p || !samples_dev) return -1;
+  return gpu_status(ipt::gpu_render_samples_sm(s, to_params(p), kd_dev, samples_dev, stream));
+}
+
+int ipt_pixel_mean_sm_dev(const float *samples_dev, int64_t npix, int spp, float *hdr_dev, uint8_t *ldr_dev,
+                          void *stream) {
+  if (!samples_dev || !hdr_dev || spp <= 0) {
+    fail("ipt_pixel_mean_sm_dev: bad arguments");
+    return -1;
+  }
+  return gpu_status(ipt::gpu_pixel_mean_sm(samples_dev, npix, spp, hdr_dev, ldr_dev, stream));
+}
+
 int ipt_adjoint_dev(void *scene, const ipt_params_t *p, const float *kd_dev, const float *adj_dev, double *grad_dev,
                     void *stream) {
   GpuScene *s = as_scene(scene);

@@ -27,6 +27,11 @@ int gpu_render_samples(GpuScene *s, const RenderParams &p, const float *kd_dev, 
                        void *stream);
 int gpu_pixel_mean(const float *samples_dev, int64_t npix, int spp, float *hdr_dev, uint8_t *ldr_dev,
                    void *stream);
+// Same pair over a sample-major buffer [s][pixel][3] (what gpu_render uses).
+int gpu_render_samples_sm(GpuScene *s, const RenderParams &p, const float *kd_dev, float *samples_dev,
+                          void *stream);
+int gpu_pixel_mean_sm(const float *samples_dev, int64_t npix, int spp, float *hdr_dev, uint8_t *ldr_dev,
+                      void *stream);
 int gpu_render(GpuScene *s, const RenderParams &p, const float *kd_dev, float *hdr_dev, uint8_t *ldr_dev,
                void *stream);
 int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const float *adj_dev,

@@ -60,6 +60,11 @@ __device__ __forceinline__ float uniform(Rng &s) {
 
 // ------------------------------------------------------------ f64 helpers
 __device__ __forceinline__ void sincos_f(float xf, float &sf, float &cf) {
+#ifdef IPT_ABL_TRIG  // timing-only ablation build
+  sf = __sinf(xf);
+  cf = __cosf(xf);
+  return;
+#endif
   const double x = (double)xf;
   const double k = rint(x * 0.6366197723675814);
   double r = fma(-k, 1.5707963267948966, x);
@@ -230,45 +235,60 @@ __device__ __forceinline__ float div_inrange(float a, float b) {
 // evaluated branch-free per lane and committed with a select.  Each skip
 // condition is written exactly as the reference's (negated) so NaNs take the
 // same branch.
-#ifndef IPT_PREFETCH
-#define IPT_PREFETCH 1
+#ifndef IPT_UNROLL2
+#define IPT_UNROLL2 0
 #endif
+// One triangle of the closest-hit loop: branch-free test, select on accept.
+__device__ __forceinline__ void hit_test(const TriIsect &T, int i, V3 p, V3 d, float &bt, int &bi) {
+  const float denom = fmaf(T.n[2], d.z, fmaf(T.n[1], d.y, T.n[0] * d.x));
+  const float px = p.x - T.c[0], py = p.y - T.c[1], pz = p.z - T.c[2];
+  const float num = fmaf(pz, T.n[2], fmaf(py, T.n[1], px * T.n[0]));
+  const float t = div_inrange(num, -denom);
+  const float qx = fmaf(d.x, t, p.x), qy = fmaf(d.y, t, p.y), qz = fmaf(d.z, t, p.z);
+  const float s0 = fmaf(qz, T.e0[2], fmaf(qy, T.e0[1], fmaf(qx, T.e0[0], T.e0[3])));
+  const float s1 = fmaf(qz, T.e1[2], fmaf(qy, T.e1[1], fmaf(qx, T.e1[0], T.e1[3])));
+  const float s2 = fmaf(qz, T.e2[2], fmaf(qy, T.e2[1], fmaf(qx, T.e2[0], T.e2[3])));
+  const bool take = !(fabsf(denom) < kMinDotUp) && !(t < kEpsUp) && !(t >= bt) && !(s0 > 0.f) &&
+                    !(s1 > 0.f) && !(s2 > 0.f);
+  bt = take ? t : bt;
+  bi = take ? i : bi;
+}
+
 __device__ __forceinline__ int closest_hit(const TriIsect *__restrict__ tris, int nT, V3 p, V3 d,
                                            float &best_t) {
   float bt = __builtin_inff();
   int bi = -1;
-#if IPT_PREFETCH
-  // software pipeline: the scalar load of record i+1 is issued before the
-  // tests of record i (SMEM returns out of order, so every wait is a full
-  // lgkmcnt(0); issuing one record ahead hides it behind ~37 VALU ops).
+  // Software pipeline: the scalar loads of the next record(s) are issued
+  // before the tests of the current one(s) -- SMEM returns out of order, so
+  // every wait is a full lgkmcnt(0) and must be covered by VALU work.
+#if IPT_UNROLL2
+  TriIsect A = tris[0], B = tris[nT > 1 ? 1 : 0];
+  int i = 0;
+  for (; i + 1 < nT; i += 2) {
+    const TriIsect cA = A, cB = B;
+    A = tris[i + 2 < nT ? i + 2 : nT - 1];
+    B = tris[i + 3 < nT ? i + 3 : nT - 1];
+    hit_test(cA, i, p, d, bt, bi);      // order kept: strict '<' prefers the first
+    hit_test(cB, i + 1, p, d, bt, bi);
+  }
+  if (i < nT) hit_test(A, i, p, d, bt, bi);
+#else
   TriIsect nxt = tris[0];
   for (int i = 0; i < nT; ++i) {
     const TriIsect T = nxt;
     nxt = tris[i + 1 < nT ? i + 1 : i];
-#else
-#pragma unroll 2
-  for (int i = 0; i < nT; ++i) {
-    const TriIsect T = tris[i];
-#endif
-    const float denom = fmaf(T.n[2], d.z, fmaf(T.n[1], d.y, T.n[0] * d.x));
-    const float px = p.x - T.c[0], py = p.y - T.c[1], pz = p.z - T.c[2];
-    const float num = fmaf(pz, T.n[2], fmaf(py, T.n[1], px * T.n[0]));
-    const float t = div_inrange(num, -denom);
-    const float qx = fmaf(d.x, t, p.x), qy = fmaf(d.y, t, p.y), qz = fmaf(d.z, t, p.z);
-    const float s0 = fmaf(qz, T.e0[2], fmaf(qy, T.e0[1], fmaf(qx, T.e0[0], T.e0[3])));
-    const float s1 = fmaf(qz, T.e1[2], fmaf(qy, T.e1[1], fmaf(qx, T.e1[0], T.e1[3])));
-    const float s2 = fmaf(qz, T.e2[2], fmaf(qy, T.e2[1], fmaf(qx, T.e2[0], T.e2[3])));
-    const bool take = !(fabsf(denom) < kMinDotUp) && !(t < kEpsUp) && !(t >= bt) && !(s0 > 0.f) &&
-                      !(s1 > 0.f) && !(s2 > 0.f);
-    bt = take ? t : bt;
-    bi = take ? i : bi;
+    hit_test(T, i, p, d, bt, bi);
   }
+#endif
   best_t = bt;
   return bi;
 }
 
 // Triangle::getNormal (scene_basics.h:100-109)
 __device__ __forceinline__ V3 shading_normal(const TriGeom &g, V3 q) {
+#ifdef IPT_ABL_NORMAL  // timing-only ablation build
+  return mk(g.vn[0][0], g.vn[0][1], g.vn[0][2]);
+#endif
   const V3 v0 = mk(g.v[0][0], g.v[0][1], g.v[0][2]);
   const V3 v1 = mk(g.v[1][0], g.v[1][1], g.v[1][2]);
   const V3 v2 = mk(g.v[2][0], g.v[2][1], g.v[2][2]);

@@ -63,20 +63,31 @@ struct TraceArgs {
   uint64_t s_begin, n_samples;
   int nT, nE;
   int lds_edges;  // GRAPH: bins privatised in LDS
+  int sample_major;  // FWD: sample buffer [s][pixel][3] (else [pixel][s][3])
+  uint64_t pix_begin, npix;
   float cam[16];
 };
 
 using namespace dev;
 
 // ---------------------------------------------------------------------------
-#ifndef IPT_MIN_BLOCKS
-#define IPT_MIN_BLOCKS 0
+// Minimum resident 256-thread blocks per CU (= waves per SIMD) requested per
+// integrator; 0 lets the compiler choose.  Measured (profiles/
+// r01_variants_occupancy.log): the forward gains from 5, the adjoint does not.
+#ifndef IPT_MIN_BLOCKS_FWD
+#define IPT_MIN_BLOCKS_FWD 5
 #endif
-#if IPT_MIN_BLOCKS > 0
-#define IPT_TRACE_BOUNDS __launch_bounds__(kBlock, IPT_MIN_BLOCKS)
-#else
-#define IPT_TRACE_BOUNDS __launch_bounds__(kBlock)
+#ifndef IPT_MIN_BLOCKS_ADJ
+#define IPT_MIN_BLOCKS_ADJ 0
 #endif
+#ifndef IPT_MIN_BLOCKS_GRAPH
+#define IPT_MIN_BLOCKS_GRAPH 0
+#endif
+template <int MODE>
+constexpr int min_blocks() {
+  return MODE == 0 ? IPT_MIN_BLOCKS_FWD : (MODE == 1 ? IPT_MIN_BLOCKS_ADJ : IPT_MIN_BLOCKS_GRAPH);
+}
+#define IPT_TRACE_BOUNDS __attribute__((amdgpu_flat_work_group_size(1, kBlock), amdgpu_waves_per_eu(min_blocks<MODE>() ? min_blocks<MODE>() : 1)))
 template <int MODE, bool SPEC>
 __global__ IPT_TRACE_BOUNDS void trace_kernel(
     const TriIsect *__restrict__ isect, const TriGeom *__restrict__ geom, const TriMat *__restrict__ mat,
@@ -197,7 +208,11 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         while (ie < nE && !(emit_cdf[ie] >= u)) ++ie;
         ie = ie < nE ? ie : nE - 1;
         const float r1 = uniform(st), r2 = uniform(st);
+#ifdef IPT_ABL_DP  // timing-only ablation build
+        const double sq = (double)sqrtf(r1);
+#else
         const double sq = sqrt((double)r1);
+#endif
         const float ca = (float)(1.0 - sq);
         const float cb = (float)(sq * (double)(1.f - r2));
         const float cc = (float)((double)r2 * sq);
@@ -220,8 +235,13 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           const float ut = uniform(st);
           float cth, sth, psamp;
           if (!spec) {
+#ifdef IPT_ABL_DP
+            cth = sqrtf(ut);
+            sth = sqrtf(1.f - ut);
+#else
             cth = (float)sqrt((double)ut);
             sth = (float)sqrt(1.0 - (double)ut);
+#endif
             psamp = kInvPiF;
           } else {
             const double cd = pow_d((double)ut, 1.0 / ((double)m.shininess + 1.0));
@@ -271,7 +291,11 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             atomicAdd(e + 6, (double)(wf * me.ke[1]));
             atomicAdd(e + 7, (double)(wf * me.ke[2]));
           } else {
+#ifdef IPT_ABL_DP
+            const float s = ((ct * ctp) / (ts * ts)) / emit_pmf[emitter];
+#else
             const float s = (float)(((double)(ct * ctp) / (td * td)) / (double)emit_pmf[emitter]);
+#endif
             lo = mk(me.ke[0] * s, me.ke[1] * s, me.ke[2] * s);
             const TriMat &m = mat[tri];
             if (SPEC && (m.flags & MAT_HAS_KS)) specd = phong(m.shininess, nh, din, sd);
@@ -319,7 +343,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     if (finished) {
       active = false;
       if (MODE == MODE_FWD) {
-        float *o = out_samples + (gidx - a.s_begin) * 3;
+        const uint64_t pixel = gidx / (uint64_t)a.spp;
+        const uint64_t slot = a.sample_major ? (gidx - pixel * a.spp) * a.npix + (pixel - a.pix_begin)
+                                             : gidx - a.s_begin;
+        float *o = out_samples + slot * 3;
         o[0] = L.x;
         o[1] = L.y;
         o[2] = L.z;
@@ -390,6 +417,32 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         if (v != 0.0) atomicAdd(dstp + i, v);
       }
     }
+  }
+}
+
+// toneMap over a sample-major buffer [s][pixel][3]: same per-pixel
+// sequential sum, but lane l reads pixel base+l, so every load of a wave is
+// one contiguous 768-byte run (the pixel-major form below strides 12*spp B).
+__global__ __launch_bounds__(kBlock) void pixel_mean_sm_kernel(const float *__restrict__ samples, int64_t npix,
+                                                               int spp, float *__restrict__ hdr,
+                                                               uint8_t *__restrict__ ldr) {
+  const int64_t px = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (px >= npix) return;
+  float tx = 0.f, ty = 0.f, tz = 0.f;
+  const float fs = (float)spp;
+  for (int i = 0; i < spp; ++i) {
+    const float *s = samples + ((int64_t)i * npix + px) * 3;
+    tx += s[0] / fs;
+    ty += s[1] / fs;
+    tz += s[2] / fs;
+  }
+  hdr[px * 3] = tx;
+  hdr[px * 3 + 1] = ty;
+  hdr[px * 3 + 2] = tz;
+  if (ldr) {
+    ldr[px * 3] = (uint8_t)(255.f * tx / (1 + tx));
+    ldr[px * 3 + 1] = (uint8_t)(255.f * ty / (1 + ty));
+    ldr[px * 3 + 2] = (uint8_t)(255.f * tz / (1 + tz));
   }
 }
 
@@ -554,6 +607,9 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.nT = s->host.nT;
   a.nE = s->host.nE;
   a.lds_edges = 0;
+  a.sample_major = 0;
+  a.pix_begin = (uint64_t)p.row_begin * p.width;
+  a.npix = (uint64_t)(p.row_end - p.row_begin) * p.width;
   std::memcpy(a.cam, s->host.cam, sizeof a.cam);
   return a;
 }
@@ -607,13 +663,31 @@ static int ensure_ws(GpuScene *s, size_t bytes) {
   return 0;
 }
 
+int gpu_render_samples_sm(GpuScene *s, const RenderParams &p, const float *kd_dev, float *samples_dev,
+                          void *stream) {
+  if (check_params(s, p)) return -1;
+  TraceArgs a = make_args(s, p);
+  a.sample_major = 1;
+  return launch<MODE_FWD>(s, a, 0, kd_dev, samples_dev, nullptr, nullptr, nullptr, nullptr, (hipStream_t)stream);
+}
+
+int gpu_pixel_mean_sm(const float *samples_dev, int64_t npix, int spp, float *hdr_dev, uint8_t *ldr_dev,
+                      void *stream) {
+  if (npix <= 0) return 0;
+  const int blocks = (int)((npix + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(pixel_mean_sm_kernel, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, samples_dev, npix,
+                     spp, hdr_dev, ldr_dev);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
 int gpu_render(GpuScene *s, const RenderParams &p, const float *kd_dev, float *hdr_dev, uint8_t *ldr_dev,
                void *stream) {
   if (check_params(s, p)) return -1;
   const int64_t npix = (int64_t)(p.row_end - p.row_begin) * p.width;
   if (ensure_ws(s, (size_t)npix * p.spp * 3 * sizeof(float))) return -1;
-  if (gpu_render_samples(s, p, kd_dev, s->ws, stream)) return -1;
-  return gpu_pixel_mean(s->ws, npix, p.spp, hdr_dev, ldr_dev, stream);
+  if (gpu_render_samples_sm(s, p, kd_dev, s->ws, stream)) return -1;
+  return gpu_pixel_mean_sm(s->ws, npix, p.spp, hdr_dev, ldr_dev, stream);
 }
 
 int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const float *adj_dev, double *grad_dev,

@@ -1,6 +1,4 @@
 set -o pipefail
 OUT=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
-timeout -k 10 300 python tools/variant_bench.py sync_b4 nospec nospec_b5 nospec_b6 > $OUT/variants_c.log 2>&1 &&
-timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider > $OUT/pytest_gpu_r01d.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY -d $OUT/pmc_sq3 -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/pmc_sq3.log 2>&1
+timeout -k 10 400 python tools/variant_bench.py cur cur4 nospec_b5 abl_norm abl_trig abl_dp abl_all > $OUT/variants_f.log 2>&1
 echo rc=$? > $OUT/cmd.status

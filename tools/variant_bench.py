@@ -25,6 +25,8 @@ SCENES["scene0"] = SCENES["cornell"] + [(A + "/shapes/cube.obj", "*Kd 0.90414629
 def load(path):
     L = C.CDLL(path, mode=os.RTLD_LOCAL)
     for name, (res, args) in N.SIGNATURES.items():
+        if not hasattr(L, name):  # older variant builds lack newer symbols
+            continue
         f = getattr(L, name)
         f.restype, f.argtypes = res, args
     return L
