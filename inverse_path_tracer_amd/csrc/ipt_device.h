@@ -289,6 +289,7 @@ __device__ __forceinline__ V3 shading_normal(const TriGeom &g, V3 q) {
 #ifdef IPT_ABL_NORMAL  // timing-only ablation build
   return mk(g.vn[0][0], g.vn[0][1], g.vn[0][2]);
 #endif
+  if (g.flags & GEOM_AXIS_FLAT) return mk(g.vn[0][0], g.vn[0][1], g.vn[0][2]);  // exact, scene_layout.h
   const V3 v0 = mk(g.v[0][0], g.v[0][1], g.v[0][2]);
   const V3 v1 = mk(g.v[1][0], g.v[1][1], g.v[1][2]);
   const V3 v2 = mk(g.v[2][0], g.v[2][1], g.v[2][2]);

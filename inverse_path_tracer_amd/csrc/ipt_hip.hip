@@ -56,6 +56,7 @@ constexpr int kBlock = 256;
 constexpr int kRecFields = 7;  // adjoint vertex record: tri, lo[3], specd, coeff, speci
 constexpr int kEdgeW = 8;      // graph bin: w, w*f, pix[3]*w*f, light[3]*w*f
 constexpr int kMaxAdjBounces = 62;
+constexpr int kMaxTableTris = 512;  // kd/kd-over-pi LDS tables up to 12 KB
 
 struct TraceArgs {
   int W, H, spp, max_bounces;
@@ -64,9 +65,24 @@ struct TraceArgs {
   int nT, nE;
   int lds_edges;  // GRAPH: bins privatised in LDS
   int sample_major;  // FWD: sample buffer [s][pixel][3] (else [pixel][s][3])
+  int kd_tables;     // kd and kd/pi staged in LDS
   uint64_t pix_begin, npix;
+  // index arithmetic: when every global sample index of the frame is below
+  // 2^32, g / spp and pixel / W use Lemire's multiply-high division
+  // (M = ceil(2^64 / d), exact for 32-bit n and d > 1) instead of the ~40
+  // instruction 64-bit division sequence
+  int idx32;
+  uint64_t m_spp, m_W;
   float cam[16];
 };
+
+__device__ __forceinline__ uint32_t udiv32(uint32_t n, uint64_t m, uint32_t d) {
+  return d == 1u ? n : (uint32_t)__umul64hi(m, (uint64_t)n);
+}
+// pixel index of global sample g
+__device__ __forceinline__ uint64_t sample_pixel(const TraceArgs &a, uint64_t g) {
+  return a.idx32 ? (uint64_t)udiv32((uint32_t)g, a.m_spp, (uint32_t)a.spp) : g / (uint64_t)a.spp;
+}
 
 using namespace dev;
 
@@ -99,17 +115,32 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   const int tid = threadIdx.x;
   const int nT = a.nT, nE = a.nE;
   const int vmax = a.max_bounces + 1;  // ADJ record capacity per lane
+  // LDS: [fp64 accumulators][kd table][kd/pi table][ADJ vertex records]
   double *lds_acc = lds;               // ADJ: nT*3 grad; GRAPH: (nT+1)*nT*kEdgeW bins
-  float *lds_rec = nullptr;
   int n_acc = 0;
   if (MODE == MODE_ADJ) {
     n_acc = nT * 3;
-    lds_rec = reinterpret_cast<float *>(lds + n_acc);
   } else if (MODE == MODE_GRAPH && a.lds_edges) {
     n_acc = (nT + 1) * nT * kEdgeW;
   }
+  // Per-triangle kd and kd/pi (the latter is BSDF's indirect `diffuse /=
+  // M_PI`, path_trace.cu:15-17): computed once per workgroup with the same
+  // IEEE division the per-vertex code would do, instead of three divisions
+  // per vertex.  Falls back to global memory for large scenes.
+  float *tab = reinterpret_cast<float *>(lds + n_acc);
+  const float *kd_t = kd;   // kd[3*tri]
+  const float *kdpi_t = tab + 3 * nT;
+  if (a.kd_tables) {
+    for (int i = tid; i < 3 * nT; i += kBlock) {
+      const float v = kd[i];
+      tab[i] = v;
+      tab[3 * nT + i] = v / kPiF;
+    }
+    kd_t = tab;
+  }
+  float *lds_rec = tab + (a.kd_tables ? 6 * nT : 0);
   for (int i = tid; i < n_acc; i += kBlock) lds_acc[i] = 0.0;
-  if (MODE != MODE_FWD) __syncthreads();
+  __syncthreads();
   double *acc = (MODE == MODE_GRAPH && !a.lds_edges) ? edges : lds_acc;
 
   // wave-uniform sample range (static partition, regenerated per lane)
@@ -146,8 +177,16 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         if (g < end) {
           gidx = g;
           rng_init(st, a.seed + g);
-          const uint64_t pixel = g / (uint64_t)a.spp;
-          const int r = (int)(pixel / (uint64_t)a.W), c = (int)(pixel % (uint64_t)a.W);
+          int r, c;
+          if (a.idx32) {
+            const uint32_t pixel = udiv32((uint32_t)g, a.m_spp, (uint32_t)a.spp);
+            r = (int)udiv32(pixel, a.m_W, (uint32_t)a.W);
+            c = (int)(pixel - (uint32_t)r * (uint32_t)a.W);
+          } else {
+            const uint64_t pixel = g / (uint64_t)a.spp;
+            r = (int)(pixel / (uint64_t)a.W);
+            c = (int)(pixel % (uint64_t)a.W);
+          }
           camera_ray(a.cam, st, r, c, a.W, a.H, p, d);
           L = mk(0.f, 0.f, 0.f);
           Le = L;
@@ -239,7 +278,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             cth = sqrtf(ut);
             sth = sqrtf(1.f - ut);
 #else
-            cth = (float)sqrt((double)ut);
+            cth = sqrtf(ut);  // == (float)sqrt((double)ut): double rounding is innocuous for sqrt
             sth = (float)sqrt(1.0 - (double)ut);
 #endif
             psamp = kInvPiF;
@@ -299,9 +338,12 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             lo = mk(me.ke[0] * s, me.ke[1] * s, me.ke[2] * s);
             const TriMat &m = mat[tri];
             if (SPEC && (m.flags & MAT_HAS_KS)) specd = phong(m.shininess, nh, din, sd);
-            const float *kdt = kd + 3 * tri;
-            Ld = mk((kdt[0] + m.ks[0] * specd) * lo.x, (kdt[1] + m.ks[1] * specd) * lo.y,
-                    (kdt[2] + m.ks[2] * specd) * lo.z);
+            const float *kdt = kd_t + 3 * tri;
+            if (SPEC)
+              Ld = mk((kdt[0] + m.ks[0] * specd) * lo.x, (kdt[1] + m.ks[1] * specd) * lo.y,
+                      (kdt[2] + m.ks[2] * specd) * lo.z);
+            else  // Ks = 0: kd + 0*0 == kd
+              Ld = mk(kdt[0] * lo.x, kdt[1] * lo.y, kdt[2] * lo.z);
           }
         }
       }
@@ -329,10 +371,16 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       } else {
         L = mk(fmaf(M.x, Le.x + Ld.x, L.x), fmaf(M.y, Le.y + Ld.y, L.y), fmaf(M.z, Le.z + Ld.z, L.z));
         if (cont) {
-          const TriMat &m = mat[tri];
-          const float *kdt = kd + 3 * tri;
-          M = mk((M.x * (kdt[0] / kPiF + m.ks[0] * speci)) * coeff, (M.y * (kdt[1] / kPiF + m.ks[1] * speci)) * coeff,
-                 (M.z * (kdt[2] / kPiF + m.ks[2] * speci)) * coeff);
+          const float *kp = a.kd_tables ? kdpi_t + 3 * tri : nullptr;
+          const float *kdt = kd_t + 3 * tri;
+          const float t0 = kp ? kp[0] : kdt[0] / kPiF, t1 = kp ? kp[1] : kdt[1] / kPiF, t2 = kp ? kp[2] : kdt[2] / kPiF;
+          if (SPEC) {
+            const TriMat &m = mat[tri];
+            M = mk((M.x * (t0 + m.ks[0] * speci)) * coeff, (M.y * (t1 + m.ks[1] * speci)) * coeff,
+                   (M.z * (t2 + m.ks[2] * speci)) * coeff);
+          } else {  // Ks = 0: kd/pi + 0*0 == kd/pi
+            M = mk((M.x * t0) * coeff, (M.y * t1) * coeff, (M.z * t2) * coeff);
+          }
         }
       }
       ++k;  // vertices so far
@@ -343,7 +391,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     if (finished) {
       active = false;
       if (MODE == MODE_FWD) {
-        const uint64_t pixel = gidx / (uint64_t)a.spp;
+        const uint64_t pixel = sample_pixel(a, gidx);
         const uint64_t slot = a.sample_major ? (gidx - pixel * a.spp) * a.npix + (pixel - a.pix_begin)
                                              : gidx - a.s_begin;
         float *o = out_samples + slot * 3;
@@ -355,31 +403,48 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         const int K = k;
         if (K > 0) {
           const size_t fs = (size_t)vmax * kBlock;
-          const uint64_t pixel = gidx / (uint64_t)a.spp;
+          const uint64_t pixel = sample_pixel(a, gidx);
           const float ax = adj[pixel * 3 + 0] / (float)a.spp;
           const float ay = adj[pixel * 3 + 1] / (float)a.spp;
           const float az = adj[pixel * 3 + 2] / (float)a.spp;
           V3 S = mk(0.f, 0.f, 0.f);
+          // T_j = kd/pi (+ Ks*speci), D_j = kd (+ Ks*specd): exactly the forward's values
+          auto tdiff = [&](int tj, float si, float &x, float &y, float &z) {
+            if (a.kd_tables) {
+              const float *kp = kdpi_t + 3 * tj;
+              x = kp[0]; y = kp[1]; z = kp[2];
+            } else {
+              const float *kq = kd + 3 * tj;
+              x = kq[0] / kPiF; y = kq[1] / kPiF; z = kq[2] / kPiF;
+            }
+            if (SPEC) {
+              const TriMat &mj = mat[tj];
+              x = x + mj.ks[0] * si; y = y + mj.ks[1] * si; z = z + mj.ks[2] * si;
+            }
+          };
+          auto ddir = [&](int tj, float sdj, float &x, float &y, float &z) {
+            const float *kq = kd_t + 3 * tj;
+            x = kq[0]; y = kq[1]; z = kq[2];
+            if (SPEC) {
+              const TriMat &mj = mat[tj];
+              x = x + mj.ks[0] * sdj; y = y + mj.ks[1] * sdj; z = z + mj.ks[2] * sdj;
+            }
+          };
           if (escaped) {
             const float *r = lds_rec + (size_t)(K - 1) * kBlock + tid;
-            const int tk = __float_as_int(r[0]);
-            const float sdk = r[4 * fs];
-            const TriMat &m = mat[tk];
-            const float *kdt = kd + 3 * tk;
-            S = mk(Le.x + (kdt[0] + m.ks[0] * sdk) * r[fs], Le.y + (kdt[1] + m.ks[1] * sdk) * r[2 * fs],
-                   Le.z + (kdt[2] + m.ks[2] * sdk) * r[3 * fs]);
+            float dx, dy, dz;
+            ddir(__float_as_int(r[0]), r[4 * fs], dx, dy, dz);
+            S = mk(Le.x + dx * r[fs], Le.y + dy * r[2 * fs], Le.z + dz * r[3 * fs]);
           }
           for (int kk = K - 1; kk >= 0; --kk) {
             // prefix throughput M_kk (recomputed exactly as the forward did)
             V3 Mk = mk(1.f, 1.f, 1.f);
             for (int j = 0; j < kk; ++j) {
               const float *rj = lds_rec + (size_t)j * kBlock + tid;
-              const int tj = __float_as_int(rj[0]);
-              const float cj = rj[5 * fs], sj = rj[6 * fs];
-              const TriMat &mj = mat[tj];
-              const float *kdj = kd + 3 * tj;
-              Mk = mk((Mk.x * (kdj[0] / kPiF + mj.ks[0] * sj)) * cj, (Mk.y * (kdj[1] / kPiF + mj.ks[1] * sj)) * cj,
-                      (Mk.z * (kdj[2] / kPiF + mj.ks[2] * sj)) * cj);
+              const float cj = rj[5 * fs];
+              float tx, ty, tz;
+              tdiff(__float_as_int(rj[0]), rj[6 * fs], tx, ty, tz);
+              Mk = mk((Mk.x * tx) * cj, (Mk.y * ty) * cj, (Mk.z * tz) * cj);
             }
             const float *r = lds_rec + (size_t)kk * kBlock + tid;
             const int tk = __float_as_int(r[0]);
@@ -397,11 +462,11 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             atomicAdd(&lds_acc[tk * 3 + 0], (double)(ax * gk.x));
             atomicAdd(&lds_acc[tk * 3 + 1], (double)(ay * gk.y));
             atomicAdd(&lds_acc[tk * 3 + 2], (double)(az * gk.z));
-            const TriMat &m = mat[tk];
-            const float *kdt = kd + 3 * tk;
-            S = mk((Le.x + (kdt[0] + m.ks[0] * sdk) * lk.x) + ((kdt[0] / kPiF + m.ks[0] * si) * ck) * S.x,
-                   (Le.y + (kdt[1] + m.ks[1] * sdk) * lk.y) + ((kdt[1] / kPiF + m.ks[1] * si) * ck) * S.y,
-                   (Le.z + (kdt[2] + m.ks[2] * sdk) * lk.z) + ((kdt[2] / kPiF + m.ks[2] * si) * ck) * S.z);
+            float dx, dy, dz, tx, ty, tz;
+            ddir(tk, sdk, dx, dy, dz);
+            tdiff(tk, si, tx, ty, tz);
+            S = mk((Le.x + dx * lk.x) + (tx * ck) * S.x, (Le.y + dy * lk.y) + (ty * ck) * S.y,
+                   (Le.z + dz * lk.z) + (tz * ck) * S.z);
           }
         }
       }
@@ -608,11 +673,18 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.nE = s->host.nE;
   a.lds_edges = 0;
   a.sample_major = 0;
+  a.kd_tables = s->host.nT <= kMaxTableTris ? 1 : 0;
   a.pix_begin = (uint64_t)p.row_begin * p.width;
   a.npix = (uint64_t)(p.row_end - p.row_begin) * p.width;
+  const uint64_t total = (uint64_t)p.height * p.width * p.spp;
+  a.idx32 = total <= 0xffffffffull ? 1 : 0;
+  a.m_spp = p.spp > 1 ? ~0ull / (uint64_t)p.spp + 1 : 0;
+  a.m_W = p.width > 1 ? ~0ull / (uint64_t)p.width + 1 : 0;
   std::memcpy(a.cam, s->host.cam, sizeof a.cam);
   return a;
 }
+
+static size_t table_bytes(const TraceArgs &a) { return a.kd_tables ? (size_t)6 * a.nT * sizeof(float) : 0; }
 
 template <int MODE, bool SPEC>
 static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float *kd_dev, float *out, const float *adj,
@@ -640,7 +712,8 @@ static int launch(GpuScene *s, const TraceArgs &a, size_t lds, const float *kd_d
 int gpu_render_samples(GpuScene *s, const RenderParams &p, const float *kd_dev, float *samples_dev, void *stream) {
   if (check_params(s, p)) return -1;
   const TraceArgs a = make_args(s, p);
-  return launch<MODE_FWD>(s, a, 0, kd_dev, samples_dev, nullptr, nullptr, nullptr, nullptr, (hipStream_t)stream);
+  return launch<MODE_FWD>(s, a, table_bytes(a), kd_dev, samples_dev, nullptr, nullptr, nullptr, nullptr,
+                          (hipStream_t)stream);
 }
 
 int gpu_pixel_mean(const float *samples_dev, int64_t npix, int spp, float *hdr_dev, uint8_t *ldr_dev, void *stream) {
@@ -668,7 +741,8 @@ int gpu_render_samples_sm(GpuScene *s, const RenderParams &p, const float *kd_de
   if (check_params(s, p)) return -1;
   TraceArgs a = make_args(s, p);
   a.sample_major = 1;
-  return launch<MODE_FWD>(s, a, 0, kd_dev, samples_dev, nullptr, nullptr, nullptr, nullptr, (hipStream_t)stream);
+  return launch<MODE_FWD>(s, a, table_bytes(a), kd_dev, samples_dev, nullptr, nullptr, nullptr, nullptr,
+                          (hipStream_t)stream);
 }
 
 int gpu_pixel_mean_sm(const float *samples_dev, int64_t npix, int spp, float *hdr_dev, uint8_t *ldr_dev,
@@ -698,7 +772,7 @@ int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const f
     return -1;
   }
   const TraceArgs a = make_args(s, p);
-  const size_t lds = (size_t)s->host.nT * 3 * sizeof(double) +
+  const size_t lds = (size_t)s->host.nT * 3 * sizeof(double) + table_bytes(a) +
                      (size_t)(p.max_bounces + 1) * kRecFields * kBlock * sizeof(float);
   if (lds > 160 * 1024) {
     gpu_set_error("adjoint LDS footprint exceeds 160 KiB; lower max_bounces");
@@ -712,6 +786,7 @@ int gpu_graph(GpuScene *s, const RenderParams &p, const uint8_t *target_dev, dou
   TraceArgs a = make_args(s, p);
   const size_t bins = (size_t)(s->host.nT + 1) * s->host.nT * kEdgeW * sizeof(double);
   a.lds_edges = bins <= 64 * 1024 ? 1 : 0;
+  a.kd_tables = 0;  // the graph integrator never reads albedo
   return launch<MODE_GRAPH>(s, a, a.lds_edges ? bins : 0, nullptr, nullptr, nullptr, nullptr, target_dev, acc_dev,
                             (hipStream_t)stream);
 }

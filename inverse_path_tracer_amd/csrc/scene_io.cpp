@@ -522,6 +522,21 @@ Tri make_tri(V3 a, V3 b, V3 c, const V3 *ns, const Material &m) {  // Triangle::
   return t;
 }
 
+// GEOM_AXIS_FLAT (scene_layout.h): equal axis-aligned vertex normals on a
+// triangle of positive finite area
+bool axis_flat(const Tri &t) {
+  if (!(t.area > 0.f) || !std::isfinite(t.area)) return false;
+  for (int j = 1; j < 3; ++j)
+    if (std::memcmp(&t.vn[j], &t.vn[0], sizeof(V3)) != 0) return false;
+  const float c[3] = {t.vn[0].x, t.vn[0].y, t.vn[0].z};
+  int zeros = 0, ones = 0;
+  for (float x : c) {
+    zeros += (x == 0.f);
+    ones += (x == 1.f || x == -1.f);
+  }
+  return zeros == 2 && ones == 1;
+}
+
 // Mesh::Mesh + ParseFromString (scene_basics.h:147-289)
 bool load_mesh(const ObjectRecord &rec, std::vector<Tri> *tris, std::string *err) {
   // T = translate(pos) * rotate(AngleAxis(|ori|, ori/|ori|)) * scale(scl)
@@ -690,6 +705,7 @@ bool build_scene(const std::vector<ObjectRecord> &objects, HostScene *out, std::
     }
     G.area = t.area;
     sampling_frame(t.n, G.R);
+    G.flags = axis_flat(t) ? GEOM_AXIS_FLAT : 0u;
     TriMat &M = S.mat[i];
     for (int j = 0; j < 3; ++j) {
       M.ks[j] = t.m.ks[j];

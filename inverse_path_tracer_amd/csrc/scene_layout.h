@@ -37,9 +37,19 @@ struct TriGeom {        // 32 floats
   float vn[3][3];       // vertex normals (columns of Triangle::normals)
   float area;
   float R[3][3];        // sampling frame, row-major (sampleNextDir)
-  float pad[4];
+  uint32_t flags;       // GEOM_AXIS_FLAT
+  float pad[3];
 };
 static_assert(sizeof(TriGeom) == 128, "TriGeom layout");
+
+// The three vertex normals are bitwise equal and axis-aligned (two components
+// +-0, one +-1).  Triangle::getNormal's blend-and-renormalise then returns that
+// normal EXACTLY: the zero components stay signed zeros, the +-1 component
+// becomes +-s with s > 0, and RN(sqrt(RN(s*s))) == s in binary IEEE
+// arithmetic, so +-s / s == +-1.  The kernels skip the blend for such
+// triangles (every Cornell wall and every cube face) -- a bitwise identity,
+// not an approximation.
+enum : uint32_t { GEOM_AXIS_FLAT = 1u };
 
 enum : uint32_t { MAT_HAS_KS = 1u, MAT_SPECULAR = 2u };
 
