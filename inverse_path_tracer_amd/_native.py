@@ -11,7 +11,9 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libipt_amd.so")
+# IPT_AMD_LIB selects another build of the same library (A/B profiling of
+# kernel variants); the default is the in-tree build.
+LIB_PATH = os.environ.get("IPT_AMD_LIB") or os.path.join(_HERE, "lib", "libipt_amd.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ipt.h")
 TRI_EXPORT_STRIDE = 57
 ACC_WIDTH = 8

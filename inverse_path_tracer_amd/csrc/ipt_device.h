@@ -284,6 +284,65 @@ __device__ __forceinline__ int closest_hit(const TriIsect *__restrict__ tris, in
   return bi;
 }
 
+#ifndef IPT_PAIRS
+#define IPT_PAIRS 1
+#endif
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 bc2(float x) { return f2{x, x}; }
+__device__ __forceinline__ f2 ld2(const TriPair &T, int k) { return f2{T.f[k][0], T.f[k][1]}; }
+
+// hit_test on triangles i (half x) and i+1 (half y) with packed FP32: the same
+// IEEE operations in the same order per half, then the two accept/select
+// steps in index order (strict '<' still prefers the first of equal t).
+__device__ __forceinline__ void hit_test_pair(const TriPair &T, int i, V3 p, V3 d, float &bt, int &bi) {
+  const f2 c0 = ld2(T, 0), c1 = ld2(T, 1), c2 = ld2(T, 2), n0 = ld2(T, 3), n1 = ld2(T, 4), n2 = ld2(T, 5);
+  const f2 denom = fma2(n2, bc2(d.z), fma2(n1, bc2(d.y), n0 * bc2(d.x)));
+  const f2 px = bc2(p.x) - c0, py = bc2(p.y) - c1, pz = bc2(p.z) - c2;
+  const f2 num = fma2(pz, n2, fma2(py, n1, px * n0));
+#if IPT_FASTDIV
+  // div_inrange(num, -denom), both halves
+  const f2 nb = denom;
+  const f2 r0 = f2{__builtin_amdgcn_rcpf(-denom.x), __builtin_amdgcn_rcpf(-denom.y)};
+  const f2 e0 = fma2(nb, r0, bc2(1.0f));
+  const f2 r1 = fma2(e0, r0, r0);
+  const f2 q0 = num * r1;
+  const f2 e1 = fma2(nb, q0, num);
+  const f2 q1 = fma2(e1, r1, q0);
+  const f2 e2 = fma2(nb, q1, num);
+  const f2 t = fma2(e2, r1, q1);
+#else
+  const f2 t = f2{num.x / -denom.x, num.y / -denom.y};
+#endif
+  const f2 qx = fma2(bc2(d.x), t, bc2(p.x)), qy = fma2(bc2(d.y), t, bc2(p.y)), qz = fma2(bc2(d.z), t, bc2(p.z));
+  const f2 s0 = fma2(qz, ld2(T, 8), fma2(qy, ld2(T, 7), fma2(qx, ld2(T, 6), ld2(T, 9))));
+  const f2 s1 = fma2(qz, ld2(T, 12), fma2(qy, ld2(T, 11), fma2(qx, ld2(T, 10), ld2(T, 13))));
+  const f2 s2 = fma2(qz, ld2(T, 16), fma2(qy, ld2(T, 15), fma2(qx, ld2(T, 14), ld2(T, 17))));
+  const bool ta = !(fabsf(denom.x) < kMinDotUp) && !(t.x < kEpsUp) && !(t.x >= bt) && !(s0.x > 0.f) &&
+                  !(s1.x > 0.f) && !(s2.x > 0.f);
+  bt = ta ? t.x : bt;
+  bi = ta ? i : bi;
+  const bool tb = !(fabsf(denom.y) < kMinDotUp) && !(t.y < kEpsUp) && !(t.y >= bt) && !(s0.y > 0.f) &&
+                  !(s1.y > 0.f) && !(s2.y > 0.f);
+  bt = tb ? t.y : bt;
+  bi = tb ? i + 1 : bi;
+}
+
+__device__ __forceinline__ int closest_hit_pairs(const TriPair *__restrict__ pairs, int nT, V3 p, V3 d,
+                                                 float &best_t) {
+  float bt = __builtin_inff();
+  int bi = -1;
+  const int nP = (nT + 1) >> 1;
+  TriPair nxt = pairs[0];
+  for (int j = 0; j < nP; ++j) {
+    const TriPair T = nxt;
+    nxt = pairs[j + 1 < nP ? j + 1 : j];
+    hit_test_pair(T, 2 * j, p, d, bt, bi);
+  }
+  best_t = bt;
+  return bi;
+}
+
 // Triangle::getNormal (scene_basics.h:100-109)
 __device__ __forceinline__ V3 shading_normal(const TriGeom &g, V3 q) {
 #ifdef IPT_ABL_NORMAL  // timing-only ablation build

@@ -72,7 +72,7 @@ struct TraceArgs {
   // (M = ceil(2^64 / d), exact for 32-bit n and d > 1) instead of the ~40
   // instruction 64-bit division sequence
   int idx32;
-  uint64_t m_spp, m_W;
+  uint64_t m_spp, m_W, m_npix;
   float cam[16];
 };
 
@@ -104,9 +104,19 @@ constexpr int min_blocks() {
   return MODE == 0 ? IPT_MIN_BLOCKS_FWD : (MODE == 1 ? IPT_MIN_BLOCKS_ADJ : IPT_MIN_BLOCKS_GRAPH);
 }
 #define IPT_TRACE_BOUNDS __attribute__((amdgpu_flat_work_group_size(1, kBlock), amdgpu_waves_per_eu(min_blocks<MODE>() ? min_blocks<MODE>() : 1)))
+__device__ __forceinline__ int cast(const TriIsect *__restrict__ isect, const TriPair *__restrict__ pairs, int nT,
+                                    V3 p, V3 d, float &t) {
+#if IPT_PAIRS
+  return closest_hit_pairs(pairs, nT, p, d, t);
+#else
+  return closest_hit(isect, nT, p, d, t);
+#endif
+}
+
 template <int MODE, bool SPEC>
 __global__ IPT_TRACE_BOUNDS void trace_kernel(
-    const TriIsect *__restrict__ isect, const TriGeom *__restrict__ geom, const TriMat *__restrict__ mat,
+    const TriIsect *__restrict__ isect, const TriPair *__restrict__ pairs, const TriGeom *__restrict__ geom,
+    const TriMat *__restrict__ mat,
     const float *__restrict__ kd, const int *__restrict__ emit_tri, const float *__restrict__ emit_cdf,
     const float *__restrict__ emit_pmf, const TraceArgs a, float *__restrict__ out_samples,
     const float *__restrict__ adj, double *__restrict__ grad, const uint8_t *__restrict__ target,
@@ -146,8 +156,14 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   // wave-uniform sample range (static partition, regenerated per lane)
   const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * kBlock + tid) >> 6);
   const uint32_t nwaves = (gridDim.x * kBlock) >> 6;
-  uint64_t next = a.s_begin + (a.n_samples * wave) / nwaves;
-  const uint64_t end = a.s_begin + (a.n_samples * (wave + 1)) / nwaves;
+  // Work items w in [0, n_samples) of this launch.  Pixel-major: w is sample
+  // g = s_begin + w (a wave traces consecutive samples of one pixel).
+  // Sample-major (FWD into a [s][pixel][3] buffer): w = s * npix + pixel, so
+  // lane i of a wave writes slot w = base + i -- one contiguous store run.
+  // Either way the sample's seed is seed + g: results do not depend on the
+  // enumeration.
+  uint64_t next = (a.n_samples * wave) / nwaves;
+  const uint64_t end = (a.n_samples * (wave + 1)) / nwaves;
 
   bool active = false;
   Rng st;
@@ -156,7 +172,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   float weight = 1.f;  // GRAPH path weight
   V3 pix = p;          // GRAPH target pixel
   int k = 0, dst = 0;
-  uint64_t gidx = 0;
+  uint64_t witem = 0;  // this lane's work item (output slot / pixel source)
 
   // One iteration = one path vertex for the whole wave, in two
   // wave-synchronous phases: (1) every active lane casts its path ray and,
@@ -173,20 +189,37 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       const uint32_t rank =
           __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
       if (!active) {
-        const uint64_t g = next + rank;
-        if (g < end) {
-          gidx = g;
-          rng_init(st, a.seed + g);
+        const uint64_t w = next + rank;
+        if (w < end) {
+          witem = w;
+          uint64_t g;
           int r, c;
           if (a.idx32) {
-            const uint32_t pixel = udiv32((uint32_t)g, a.m_spp, (uint32_t)a.spp);
+            uint32_t pixel;
+            if (a.sample_major) {
+              const uint32_t sj = udiv32((uint32_t)w, a.m_npix, (uint32_t)a.npix);
+              pixel = (uint32_t)a.pix_begin + ((uint32_t)w - sj * (uint32_t)a.npix);
+              g = (uint64_t)pixel * (uint32_t)a.spp + sj;
+            } else {
+              g = a.s_begin + w;
+              pixel = udiv32((uint32_t)g, a.m_spp, (uint32_t)a.spp);
+            }
             r = (int)udiv32(pixel, a.m_W, (uint32_t)a.W);
             c = (int)(pixel - (uint32_t)r * (uint32_t)a.W);
           } else {
-            const uint64_t pixel = g / (uint64_t)a.spp;
+            uint64_t pixel;
+            if (a.sample_major) {
+              const uint64_t sj = w / a.npix;
+              pixel = a.pix_begin + (w - sj * a.npix);
+              g = pixel * (uint64_t)a.spp + sj;
+            } else {
+              g = a.s_begin + w;
+              pixel = g / (uint64_t)a.spp;
+            }
             r = (int)(pixel / (uint64_t)a.W);
             c = (int)(pixel % (uint64_t)a.W);
           }
+          rng_init(st, a.seed + g);
           camera_ray(a.cam, st, r, c, a.W, a.H, p, d);
           L = mk(0.f, 0.f, 0.f);
           Le = L;
@@ -209,7 +242,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     // ================= phase 1: path ray (radiance, path_trace.cu:111-144)
     float t = 0.f;
     int hit = -1;
-    if (active) hit = closest_hit(isect, nT, p, d, t);
+    if (active) hit = cast(isect, pairs, nT, p, d, t);
     const bool vertex = active && hit >= 0;
     bool finished = false, escaped = false;
     if (active && hit < 0) {  // miss: the stale L_e/L_d are re-added (F4)
@@ -309,7 +342,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     if (__ballot(shadow)) {
       float ts = 0.f;
       int hs = -1;
-      if (shadow) hs = closest_hit(isect, nT, p, sd, ts);
+      if (shadow) hs = cast(isect, pairs, nT, p, sd, ts);
       const int et = shadow ? emit_tri[emitter] : -1;
       if (shadow && hs == et) {  // must hit the sampled emitter itself
         const V3 ne = shading_normal(geom[et], along(p, sd, ts));
@@ -391,10 +424,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     if (finished) {
       active = false;
       if (MODE == MODE_FWD) {
-        const uint64_t pixel = sample_pixel(a, gidx);
-        const uint64_t slot = a.sample_major ? (gidx - pixel * a.spp) * a.npix + (pixel - a.pix_begin)
-                                             : gidx - a.s_begin;
-        float *o = out_samples + slot * 3;
+        float *o = out_samples + witem * 3;
         o[0] = L.x;
         o[1] = L.y;
         o[2] = L.z;
@@ -403,7 +433,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         const int K = k;
         if (K > 0) {
           const size_t fs = (size_t)vmax * kBlock;
-          const uint64_t pixel = sample_pixel(a, gidx);
+          const uint64_t pixel = sample_pixel(a, a.s_begin + witem);  // pixel-major
           const float ax = adj[pixel * 3 + 0] / (float)a.spp;
           const float ay = adj[pixel * 3 + 1] / (float)a.spp;
           const float az = adj[pixel * 3 + 2] / (float)a.spp;
@@ -541,6 +571,7 @@ struct GpuScene {
   int device = 0;
   bool on_device = false;
   TriIsect *isect = nullptr;
+  TriPair *pairs = nullptr;
   TriGeom *geom = nullptr;
   TriMat *mat = nullptr;
   float *kd = nullptr;
@@ -572,7 +603,9 @@ GpuScene *gpu_upload(const HostScene &host, std::string *err) {
     delete s;
     return nullptr;
   }
-  if (upload(&s->isect, host.isect) || upload(&s->geom, host.geom) || upload(&s->mat, host.mat) ||
+  std::vector<TriPair> pairs((host.isect.size() + 1) / 2);
+  pack_pairs(host.isect.data(), (int)host.isect.size(), pairs.data());
+  if (upload(&s->isect, host.isect) || upload(&s->pairs, pairs) || upload(&s->geom, host.geom) || upload(&s->mat, host.mat) ||
       upload(&s->kd, host.kd) || upload(&s->emit_tri, host.emit_tri) || upload(&s->emit_cdf, host.emit_cdf) ||
       upload(&s->emit_pmf, host.emit_pmf)) {
     *err = gpu_last_error();
@@ -598,6 +631,7 @@ void gpu_free(GpuScene *s) {
     return;
   }
   (void)hipFree(s->isect);
+  (void)hipFree(s->pairs);
   (void)hipFree(s->geom);
   (void)hipFree(s->mat);
   (void)hipFree(s->kd);
@@ -680,6 +714,7 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.idx32 = total <= 0xffffffffull ? 1 : 0;
   a.m_spp = p.spp > 1 ? ~0ull / (uint64_t)p.spp + 1 : 0;
   a.m_W = p.width > 1 ? ~0ull / (uint64_t)p.width + 1 : 0;
+  a.m_npix = a.npix > 1 ? ~0ull / a.npix + 1 : 0;
   std::memcpy(a.cam, s->host.cam, sizeof a.cam);
   return a;
 }
@@ -692,7 +727,7 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
   int grid = 0;
   if (resident_grid<MODE, SPEC>(s, lds, &grid)) return -1;
   if (a.n_samples == 0) return 0;
-  hipLaunchKernelGGL((trace_kernel<MODE, SPEC>), dim3(grid), dim3(kBlock), lds, st, s->isect, s->geom, s->mat,
+  hipLaunchKernelGGL((trace_kernel<MODE, SPEC>), dim3(grid), dim3(kBlock), lds, st, s->isect, s->pairs, s->geom, s->mat,
                      kd_dev ? kd_dev : s->kd, s->emit_tri, s->emit_cdf, s->emit_pmf, a, out, adj, grad, target,
                      edges);
   HIP_TRY(hipGetLastError());

@@ -32,6 +32,32 @@ struct TriIsect {       // 20 floats
 };
 static_assert(sizeof(TriIsect) == 80, "TriIsect layout");
 
+// Two consecutive triangles (2j, 2j+1) field-interleaved: every field is an
+// (A, B) float pair, i.e. one 64-bit SGPR pair after the scalar load, which
+// is exactly the operand a packed-FP32 instruction (v_pk_fma_f32) takes -- the
+// closest-hit loop tests both triangles with one instruction per field.
+// Field order: c[3], n[3], e0[4], e1[4], e2[4].  An odd count is padded with
+// an all-zero triangle, which the |n.d| < eps test always rejects.
+struct TriPair {
+  float f[18][2];
+};
+static_assert(sizeof(TriPair) == 144, "TriPair layout");
+inline void pack_pairs(const TriIsect *t, int nT, TriPair *out) {
+  for (int j = 0; 2 * j < nT; ++j) {
+    for (int h = 0; h < 2; ++h) {
+      const int i = 2 * j + h;
+      float src[18] = {0.f};
+      if (i < nT) {
+        const TriIsect &T = t[i];
+        const float v[18] = {T.c[0], T.c[1], T.c[2], T.n[0], T.n[1], T.n[2], T.e0[0], T.e0[1], T.e0[2],
+                             T.e0[3], T.e1[0], T.e1[1], T.e1[2], T.e1[3], T.e2[0], T.e2[1], T.e2[2], T.e2[3]};
+        for (int k = 0; k < 18; ++k) src[k] = v[k];
+      }
+      for (int k = 0; k < 18; ++k) out[j].f[k][h] = src[k];
+    }
+  }
+}
+
 struct TriGeom {        // 32 floats
   float v[3][3];        // vertices
   float vn[3][3];       // vertex normals (columns of Triangle::normals)

@@ -293,6 +293,24 @@ def test_sample_major_buffer_and_mean(scenes, oracle):
     assert np.array_equal(bits(hdr.cpu().numpy()), bits(hq))
 
 
+@pytest.mark.parametrize("W,H,spp,rows", [(512, 512, 64, None), (333, 97, 7, (13, 90))])
+def test_sample_major_equals_pixel_major_at_c2_size(scenes, W, H, spp, rows):
+    """The two sample layouts hold the same bits (work enumeration does not
+    change any sample), at the bench's full C2 size and on an odd band."""
+    from inverse_path_tracer_amd import _native as N
+
+    P, _ = scenes["cornell"]
+    p = N.make_params(W, H, spp, 4, 99, *(rows or (0, H)))
+    npix = (p.row_end - p.row_begin) * W
+    a = torch.empty((npix, spp, 3), device="cuda")
+    b = torch.empty((spp, npix, 3), device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    N.check(N.lib().ipt_render_samples_dev(P.handle, C.byref(p), None, a.data_ptr(), st))
+    N.check(N.lib().ipt_render_samples_sm_dev(P.handle, C.byref(p), None, b.data_ptr(), st))
+    torch.cuda.synchronize()
+    assert torch.equal(a.view(torch.int32), b.permute(1, 0, 2).contiguous().view(torch.int32))
+
+
 def test_material_recovery_c5_small():
     """C5 in miniature: Adam through the adjoint recovers the cube's albedo."""
     import os
@@ -310,7 +328,7 @@ def test_material_recovery_c5_small():
         img = torch_ops.render(t.scene, t.kd, 64, 64, 64, 4, seed=5)
         ((img - t.target) ** 2).mean().backward()
         g = t.kd.grad.abs().sum(1)[18:]
-        masks.append(g > 0.05 * float(g.max()))
+        masks.append(g > 0.25 * float(g.max()))
         t.kd.grad = None
     err0 = [float((t.kd.detach() - t.truth)[18:][m].abs().mean()) for t, m in zip(tasks, masks)]
     optimize(tasks, 64, 64, 16, 4, steps=60, lr=2e-2)

@@ -68,15 +68,20 @@ def main():
         buf = torch.empty((512 * 512 * 64, 3), device=dev)
         adj = torch.ones((512, 512, 3), device=dev)
         g = torch.zeros((64, 3), dtype=torch.float64, device=dev)
-        times = {n: {"fwd": [], "adj": []} for n in libs}
+        kinds = ("fwd", "fsm", "adj")
+        times = {n: {k: [] for k in kinds} for n in libs}
         for rnd in range(6):
             for n, L in libs.items():
-                for kind in ("fwd", "adj"):
+                for kind in kinds:
+                    if kind == "fsm" and not hasattr(L, "ipt_render_samples_sm_dev"):
+                        continue
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
                     for _ in range(3):
                         if kind == "fwd":
                             assert L.ipt_render_samples_dev(hs[n], C.byref(p), None, buf.data_ptr(), st) == 0
+                        elif kind == "fsm":
+                            assert L.ipt_render_samples_sm_dev(hs[n], C.byref(p), None, buf.data_ptr(), st) == 0
                         else:
                             assert L.ipt_adjoint_dev(hs[n], C.byref(p), None, adj.data_ptr(), g.data_ptr(), st) == 0
                     e1.record()
@@ -85,7 +90,8 @@ def main():
                         times[n][kind].append(e0.elapsed_time(e1) / 3)
         for n in libs:
             f, a = np.median(times[n]["fwd"]), np.median(times[n]["adj"])
-            out[sname + ":" + n] = {"fwd_ms": round(f, 4), "adj_ms": round(a, 4),
+            fs = np.median(times[n]["fsm"]) if times[n]["fsm"] else float("nan")
+            out[sname + ":" + n] = {"fwd_ms": round(f, 4), "fsm_ms": round(fs, 4), "adj_ms": round(a, 4),
                                     "fwd_Msps": round(512 * 512 * 64 / f / 1e3, 1), "adj_Msps": round(512 * 512 * 64 / a / 1e3, 1)}
             print(sname, n, out[sname + ":" + n], flush=True)
     print(json.dumps(out))
