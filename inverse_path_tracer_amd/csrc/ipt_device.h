@@ -287,6 +287,9 @@ __device__ __forceinline__ int closest_hit(const TriIsect *__restrict__ tris, in
 #ifndef IPT_PAIRS
 #define IPT_PAIRS 1
 #endif
+#ifndef IPT_PAIR_UNROLL
+#define IPT_PAIR_UNROLL 1
+#endif
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f2 bc2(float x) { return f2{x, x}; }
@@ -333,12 +336,22 @@ __device__ __forceinline__ int closest_hit_pairs(const TriPair *__restrict__ pai
   float bt = __builtin_inff();
   int bi = -1;
   const int nP = (nT + 1) >> 1;
+#if IPT_PAIR_UNROLL == 2
+  int j = 0;
+  for (; j + 1 < nP; j += 2) {
+    const TriPair A = pairs[j], B = pairs[j + 1];
+    hit_test_pair(A, 2 * j, p, d, bt, bi);
+    hit_test_pair(B, 2 * j + 2, p, d, bt, bi);
+  }
+  if (j < nP) hit_test_pair(pairs[j], 2 * j, p, d, bt, bi);
+#else
   TriPair nxt = pairs[0];
   for (int j = 0; j < nP; ++j) {
     const TriPair T = nxt;
     nxt = pairs[j + 1 < nP ? j + 1 : j];
     hit_test_pair(T, 2 * j, p, d, bt, bi);
   }
+#endif
   best_t = bt;
   return bi;
 }

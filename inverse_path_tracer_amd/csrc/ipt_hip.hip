@@ -104,6 +104,21 @@ constexpr int min_blocks() {
   return MODE == 0 ? IPT_MIN_BLOCKS_FWD : (MODE == 1 ? IPT_MIN_BLOCKS_ADJ : IPT_MIN_BLOCKS_GRAPH);
 }
 #define IPT_TRACE_BOUNDS __attribute__((amdgpu_flat_work_group_size(1, kBlock), amdgpu_waves_per_eu(min_blocks<MODE>() ? min_blocks<MODE>() : 1)))
+// Profiling-only build (make variant DEFS=-DIPT_PHASE_TIMING): each wave
+// accumulates s_memtime cycles per phase of the loop; read with
+// ipt_debug_phase_cycles (tools/phase_timing.py).
+#ifdef IPT_PHASE_TIMING
+__device__ unsigned long long g_phase_cycles[8];
+#define PHASE(i)                                     \
+  {                                                  \
+    const uint64_t tn_ = __builtin_amdgcn_s_memtime(); \
+    tacc[i] += tn_ - tp_;                            \
+    tp_ = tn_;                                       \
+  }
+#else
+#define PHASE(i)
+#endif
+
 __device__ __forceinline__ int cast(const TriIsect *__restrict__ isect, const TriPair *__restrict__ pairs, int nT,
                                     V3 p, V3 d, float &t) {
 #if IPT_PAIRS
@@ -182,6 +197,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   // then every vertex lane finalises (L, M, records, next ray).  Each shading
   // block thus runs once per vertex with most lanes on, instead of path and
   // shadow lanes serialising each other's code every iteration.
+#ifdef IPT_PHASE_TIMING
+  uint64_t tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t tp_ = __builtin_amdgcn_s_memtime();
+#endif
   for (;;) {
     // ---- refill finished lanes from the wave's range (ballot + mbcnt)
     const uint64_t need = __ballot(!active);
@@ -237,12 +256,18 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       }
       next += (uint64_t)__popcll(need);
     }
+    PHASE(0)
     if (__ballot(active) == 0) break;
+#ifdef IPT_PHASE_TIMING
+    tacc[6] += 1;
+    tacc[7] += __popcll(__ballot(active));
+#endif
 
     // ================= phase 1: path ray (radiance, path_trace.cu:111-144)
     float t = 0.f;
     int hit = -1;
     if (active) hit = cast(isect, pairs, nT, p, d, t);
+    PHASE(1)
     const bool vertex = active && hit >= 0;
     bool finished = false, escaped = false;
     if (active && hit < 0) {  // miss: the stale L_e/L_d are re-added (F4)
@@ -338,11 +363,13 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     }
 
     // ================= phase 2: next-event shadow ray (path_trace.cu:73-88)
+    PHASE(2)
     V3 lo = mk(0.f, 0.f, 0.f);
     if (__ballot(shadow)) {
       float ts = 0.f;
       int hs = -1;
       if (shadow) hs = cast(isect, pairs, nT, p, sd, ts);
+      PHASE(3)
       const int et = shadow ? emit_tri[emitter] : -1;
       if (shadow && hs == et) {  // must hit the sampled emitter itself
         const V3 ne = shading_normal(geom[et], along(p, sd, ts));
@@ -382,6 +409,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       }
     }
 
+    PHASE(4)
     // ================= finalise the vertex
     if (vertex) {
       if (MODE == MODE_ADJ) {  // vertex record k (layout [field][vertex][lane])
@@ -501,7 +529,12 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         }
       }
     }
+    PHASE(5)
   }
+#ifdef IPT_PHASE_TIMING
+  if ((tid & 63) == 0)
+    for (int i = 0; i < 8; ++i) atomicAdd(&g_phase_cycles[i], (unsigned long long)tacc[i]);
+#endif
 
   if (MODE != MODE_FWD) {
     __syncthreads();
@@ -583,6 +616,14 @@ struct GpuScene {
   int grid[6] = {0, 0, 0, 0, 0, 0};  // resident workgroups per (mode, spec) (0 = not queried)
   size_t grid_lds[6] = {0, 0, 0, 0, 0, 0};
 };
+
+#ifdef IPT_PHASE_TIMING
+extern "C" int ipt_debug_phase_cycles(unsigned long long *out) {  // read and reset
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#endif
 
 const HostScene &gpu_host(const GpuScene *s) { return s->host; }
 HostScene &gpu_host_mut(GpuScene *s) { return s->host; }
