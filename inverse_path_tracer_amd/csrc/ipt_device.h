@@ -298,11 +298,23 @@ __device__ __forceinline__ f2 ld2(const TriPair &T, int k) { return f2{T.f[k][0]
 // hit_test on triangles i (half x) and i+1 (half y) with packed FP32: the same
 // IEEE operations in the same order per half, then the two accept/select
 // steps in index order (strict '<' still prefers the first of equal t).
-__device__ __forceinline__ void hit_test_pair(const TriPair &T, int i, V3 p, V3 d, float &bt, int &bi) {
+struct PairOrigin {
+  f2 px, py, pz, num;
+};
+__device__ __forceinline__ PairOrigin pair_origin(const TriPair &T, V3 p) {
   const f2 c0 = ld2(T, 0), c1 = ld2(T, 1), c2 = ld2(T, 2), n0 = ld2(T, 3), n1 = ld2(T, 4), n2 = ld2(T, 5);
+  PairOrigin o;
+  o.px = bc2(p.x) - c0;
+  o.py = bc2(p.y) - c1;
+  o.pz = bc2(p.z) - c2;
+  o.num = fma2(o.pz, n2, fma2(o.py, n1, o.px * n0));
+  return o;
+}
+__device__ __forceinline__ void pair_ray(const TriPair &T, const PairOrigin &o, int i, V3 p, V3 d, float &bt,
+                                         int &bi, f2 e03, f2 e13, f2 e23) {
+  const f2 n0 = ld2(T, 3), n1 = ld2(T, 4), n2 = ld2(T, 5);
   const f2 denom = fma2(n2, bc2(d.z), fma2(n1, bc2(d.y), n0 * bc2(d.x)));
-  const f2 px = bc2(p.x) - c0, py = bc2(p.y) - c1, pz = bc2(p.z) - c2;
-  const f2 num = fma2(pz, n2, fma2(py, n1, px * n0));
+  const f2 num = o.num;
 #if IPT_FASTDIV
   // div_inrange(num, -denom), both halves
   const f2 nb = denom;
@@ -318,9 +330,9 @@ __device__ __forceinline__ void hit_test_pair(const TriPair &T, int i, V3 p, V3 
   const f2 t = f2{num.x / -denom.x, num.y / -denom.y};
 #endif
   const f2 qx = fma2(bc2(d.x), t, bc2(p.x)), qy = fma2(bc2(d.y), t, bc2(p.y)), qz = fma2(bc2(d.z), t, bc2(p.z));
-  const f2 s0 = fma2(qz, ld2(T, 8), fma2(qy, ld2(T, 7), fma2(qx, ld2(T, 6), ld2(T, 9))));
-  const f2 s1 = fma2(qz, ld2(T, 12), fma2(qy, ld2(T, 11), fma2(qx, ld2(T, 10), ld2(T, 13))));
-  const f2 s2 = fma2(qz, ld2(T, 16), fma2(qy, ld2(T, 15), fma2(qx, ld2(T, 14), ld2(T, 17))));
+  const f2 s0 = fma2(qz, ld2(T, 8), fma2(qy, ld2(T, 7), fma2(qx, ld2(T, 6), e03)));
+  const f2 s1 = fma2(qz, ld2(T, 12), fma2(qy, ld2(T, 11), fma2(qx, ld2(T, 10), e13)));
+  const f2 s2 = fma2(qz, ld2(T, 16), fma2(qy, ld2(T, 15), fma2(qx, ld2(T, 14), e23)));
   const bool ta = !(fabsf(denom.x) < kMinDotUp) && !(t.x < kEpsUp) && !(t.x >= bt) && !(s0.x > 0.f) &&
                   !(s1.x > 0.f) && !(s2.x > 0.f);
   bt = ta ? t.x : bt;
@@ -329,6 +341,32 @@ __device__ __forceinline__ void hit_test_pair(const TriPair &T, int i, V3 p, V3 
                   !(s1.y > 0.f) && !(s2.y > 0.f);
   bt = tb ? t.y : bt;
   bi = tb ? i + 1 : bi;
+}
+__device__ __forceinline__ void hit_test_pair(const TriPair &T, int i, V3 p, V3 d, float &bt, int &bi) {
+  pair_ray(T, pair_origin(T, p), i, p, d, bt, bi, ld2(T, 9), ld2(T, 13), ld2(T, 17));
+}
+
+// Small scenes (nT <= 2 * kSmallPairs): the pair loop fully unrolled, and the
+// three edge-plane offsets of each pair read from an LDS copy (e3[3j + k] =
+// pair j's plane-k offset).  fma(q, e_k0, e_k3) has two wave-uniform operands,
+// which the constant bus cannot feed to one VOP3P instruction, so from SGPRs
+// each costs two v_mov; from LDS (immediate offsets) it costs no VALU.  The
+// unrolled triangle index is an inline constant (no v_mov either).
+constexpr int kSmallPairs = 16;
+__device__ __forceinline__ int closest_hit_pairs_small(const TriPair *__restrict__ pairs, const f2 *e3, int nT,
+                                                       V3 p, V3 d, float &best_t) {
+  float bt = __builtin_inff();
+  int bi = -1;
+  const int nP = (nT + 1) >> 1;
+#pragma unroll
+  for (int j = 0; j < kSmallPairs; ++j) {
+    if (j < nP) {  // wave-uniform
+      const TriPair T = pairs[j];
+      pair_ray(T, pair_origin(T, p), 2 * j, p, d, bt, bi, e3[3 * j], e3[3 * j + 1], e3[3 * j + 2]);
+    }
+  }
+  best_t = bt;
+  return bi;
 }
 
 __device__ __forceinline__ int closest_hit_pairs(const TriPair *__restrict__ pairs, int nT, V3 p, V3 d,

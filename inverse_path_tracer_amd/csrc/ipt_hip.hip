@@ -66,6 +66,7 @@ struct TraceArgs {
   int lds_edges;  // GRAPH: bins privatised in LDS
   int sample_major;  // FWD: sample buffer [s][pixel][3] (else [pixel][s][3])
   int kd_tables;     // kd and kd/pi staged in LDS
+  int small_pairs;   // nT <= 2*kSmallPairs: unrolled closest-hit, plane offsets in LDS
   uint64_t pix_begin, npix;
   // index arithmetic: when every global sample index of the frame is below
   // 2^32, g / spp and pixel / W use Lemire's multiply-high division
@@ -119,9 +120,15 @@ __device__ unsigned long long g_phase_cycles[8];
 #define PHASE(i)
 #endif
 
-__device__ __forceinline__ int cast(const TriIsect *__restrict__ isect, const TriPair *__restrict__ pairs, int nT,
-                                    V3 p, V3 d, float &t) {
+#ifndef IPT_SMALL_UNROLL
+#define IPT_SMALL_UNROLL 1
+#endif
+__device__ __forceinline__ int cast(const TriIsect *__restrict__ isect, const TriPair *__restrict__ pairs,
+                                    const f2 *e3, int nT, V3 p, V3 d, float &t) {
 #if IPT_PAIRS
+#if IPT_SMALL_UNROLL
+  if (e3) return closest_hit_pairs_small(pairs, e3, nT, p, d, t);
+#endif
   return closest_hit_pairs(pairs, nT, p, d, t);
 #else
   return closest_hit(isect, nT, p, d, t);
@@ -163,7 +170,19 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     }
     kd_t = tab;
   }
-  float *lds_rec = tab + (a.kd_tables ? 6 * nT : 0);
+  // edge-plane offsets of each triangle pair for the unrolled small-scene
+  // closest-hit loop (ipt_device.h::closest_hit_pairs_small)
+  const f2 *e3 = nullptr;
+  float *lds_e3 = tab + (a.kd_tables ? 6 * nT : 0);
+  const int nP = (nT + 1) >> 1;
+  if (a.small_pairs) {
+    for (int i = tid; i < 6 * nP; i += kBlock) {
+      const int j = i / 6, kf = (i % 6) >> 1, h = i & 1;
+      lds_e3[i] = pairs[j].f[9 + 4 * kf][h];
+    }
+    e3 = reinterpret_cast<const f2 *>(lds_e3);
+  }
+  float *lds_rec = lds_e3 + (a.small_pairs ? 6 * nP : 0);
   for (int i = tid; i < n_acc; i += kBlock) lds_acc[i] = 0.0;
   __syncthreads();
   double *acc = (MODE == MODE_GRAPH && !a.lds_edges) ? edges : lds_acc;
@@ -266,7 +285,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     // ================= phase 1: path ray (radiance, path_trace.cu:111-144)
     float t = 0.f;
     int hit = -1;
-    if (active) hit = cast(isect, pairs, nT, p, d, t);
+    if (active) hit = cast(isect, pairs, e3, nT, p, d, t);
     PHASE(1)
     const bool vertex = active && hit >= 0;
     bool finished = false, escaped = false;
@@ -368,7 +387,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     if (__ballot(shadow)) {
       float ts = 0.f;
       int hs = -1;
-      if (shadow) hs = cast(isect, pairs, nT, p, sd, ts);
+      if (shadow) hs = cast(isect, pairs, e3, nT, p, sd, ts);
       PHASE(3)
       const int et = shadow ? emit_tri[emitter] : -1;
       if (shadow && hs == et) {  // must hit the sampled emitter itself
@@ -749,6 +768,7 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.lds_edges = 0;
   a.sample_major = 0;
   a.kd_tables = s->host.nT <= kMaxTableTris ? 1 : 0;
+  a.small_pairs = (IPT_PAIRS && IPT_SMALL_UNROLL && s->host.nT <= 2 * kSmallPairs) ? 1 : 0;
   a.pix_begin = (uint64_t)p.row_begin * p.width;
   a.npix = (uint64_t)(p.row_end - p.row_begin) * p.width;
   const uint64_t total = (uint64_t)p.height * p.width * p.spp;
@@ -760,7 +780,10 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   return a;
 }
 
-static size_t table_bytes(const TraceArgs &a) { return a.kd_tables ? (size_t)6 * a.nT * sizeof(float) : 0; }
+static size_t table_bytes(const TraceArgs &a) {
+  return (a.kd_tables ? (size_t)6 * a.nT * sizeof(float) : 0) +
+         (a.small_pairs ? (size_t)6 * ((a.nT + 1) / 2) * sizeof(float) : 0);
+}
 
 template <int MODE, bool SPEC>
 static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float *kd_dev, float *out, const float *adj,
@@ -863,7 +886,7 @@ int gpu_graph(GpuScene *s, const RenderParams &p, const uint8_t *target_dev, dou
   const size_t bins = (size_t)(s->host.nT + 1) * s->host.nT * kEdgeW * sizeof(double);
   a.lds_edges = bins <= 64 * 1024 ? 1 : 0;
   a.kd_tables = 0;  // the graph integrator never reads albedo
-  return launch<MODE_GRAPH>(s, a, a.lds_edges ? bins : 0, nullptr, nullptr, nullptr, nullptr, target_dev, acc_dev,
+  return launch<MODE_GRAPH>(s, a, (a.lds_edges ? bins : 0) + table_bytes(a), nullptr, nullptr, nullptr, nullptr, target_dev, acc_dev,
                             (hipStream_t)stream);
 }
 
