@@ -59,6 +59,16 @@ __device__ __forceinline__ float uniform(Rng &s) {
 }
 
 // ------------------------------------------------------------ f64 helpers
+// A double constant materialised into an SGPR pair at its point of use.  The
+// megakernel loop is long and register-bound: left alone, the compiler hoists
+// the 21 sin/cos coefficients out of it into VGPR pairs, runs out of VGPRs and
+// spills them to scratch, reloading each (with a full vmcnt wait) inside the
+// polynomial.  As SGPR operands they cost two s_mov per use on the scalar pipe.
+__device__ __forceinline__ double kc(double c) {
+  asm volatile("" : "+s"(c));
+  return c;
+}
+
 __device__ __forceinline__ void sincos_f(float xf, float &sf, float &cf) {
 #ifdef IPT_ABL_TRIG  // timing-only ablation build
   sf = __sinf(xf);
@@ -66,28 +76,28 @@ __device__ __forceinline__ void sincos_f(float xf, float &sf, float &cf) {
   return;
 #endif
   const double x = (double)xf;
-  const double k = rint(x * 0.6366197723675814);
-  double r = fma(-k, 1.5707963267948966, x);
-  r = fma(-k, 6.123233995736766e-17, r);
+  const double k = rint(x * kc(0.6366197723675814));
+  double r = fma(-k, kc(1.5707963267948966), x);
+  r = fma(-k, kc(6.123233995736766e-17), r);
   const double z = r * r;
-  double ps = 2.8114572543455206e-15;
-  ps = fma(ps, z, -7.647163731819816e-13);
-  ps = fma(ps, z, 1.6059043836821613e-10);
-  ps = fma(ps, z, -2.505210838544172e-08);
-  ps = fma(ps, z, 2.7557319223985893e-06);
-  ps = fma(ps, z, -0.0001984126984126984);
-  ps = fma(ps, z, 0.008333333333333333);
-  ps = fma(ps, z, -0.16666666666666666);
+  double ps = kc(2.8114572543455206e-15);
+  ps = fma(ps, z, kc(-7.647163731819816e-13));
+  ps = fma(ps, z, kc(1.6059043836821613e-10));
+  ps = fma(ps, z, kc(-2.505210838544172e-08));
+  ps = fma(ps, z, kc(2.7557319223985893e-06));
+  ps = fma(ps, z, kc(-0.0001984126984126984));
+  ps = fma(ps, z, kc(0.008333333333333333));
+  ps = fma(ps, z, kc(-0.16666666666666666));
   const double s = fma(ps * z, r, r);
-  double pc = -1.5619206968586225e-16;
-  pc = fma(pc, z, 4.779477332387385e-14);
-  pc = fma(pc, z, -1.1470745597729725e-11);
-  pc = fma(pc, z, 2.08767569878681e-09);
-  pc = fma(pc, z, -2.755731922398589e-07);
-  pc = fma(pc, z, 2.48015873015873e-05);
-  pc = fma(pc, z, -0.001388888888888889);
-  pc = fma(pc, z, 0.041666666666666664);
-  pc = fma(pc, z, -0.5);
+  double pc = kc(-1.5619206968586225e-16);
+  pc = fma(pc, z, kc(4.779477332387385e-14));
+  pc = fma(pc, z, kc(-1.1470745597729725e-11));
+  pc = fma(pc, z, kc(2.08767569878681e-09));
+  pc = fma(pc, z, kc(-2.755731922398589e-07));
+  pc = fma(pc, z, kc(2.48015873015873e-05));
+  pc = fma(pc, z, kc(-0.001388888888888889));
+  pc = fma(pc, z, kc(0.041666666666666664));
+  pc = fma(pc, z, kc(-0.5));
   const double c = fma(pc, z, 1.0);
   const int q = ((int)k) & 3;
   const double so = (q == 0) ? s : (q == 1) ? c : (q == 2) ? -s : -c;

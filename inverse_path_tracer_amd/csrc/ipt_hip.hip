@@ -53,7 +53,11 @@ const char *gpu_last_error() { return g_gpu_err.c_str(); }
 
 enum { MODE_FWD = 0, MODE_ADJ = 1, MODE_GRAPH = 2 };
 constexpr int kBlock = 256;
-constexpr int kRecFields = 7;  // adjoint vertex record: tri, lo[3], specd, coeff, speci
+// Adjoint vertex record (per lane, in LDS): tri | et << 16, the emitter factor
+// s (lo = Ke[et] * s is rebuilt bit-identically in the sweep; s = 0 when the
+// shadow ray failed), coeff; with a Phong lobe also specd and speci.
+constexpr int kRecFieldsDiffuse = 3, kRecFieldsSpec = 5;
+constexpr int kMaxAdjTris = 65535;  // tri and et share one 32-bit field
 constexpr int kEdgeW = 8;      // graph bin: w, w*f, pix[3]*w*f, light[3]*w*f
 constexpr int kMaxAdjBounces = 62;
 constexpr int kMaxTableTris = 512;  // kd/kd-over-pi LDS tables up to 12 KB
@@ -90,12 +94,13 @@ using namespace dev;
 // ---------------------------------------------------------------------------
 // Minimum resident 256-thread blocks per CU (= waves per SIMD) requested per
 // integrator; 0 lets the compiler choose.  Measured (profiles/
-// r01_variants_occupancy.log): the forward gains from 5, the adjoint does not.
+// r01_variants_*.log): 6 for the forward (80 VGPRs, 20 B of cold spill) and
+// the adjoint (80 VGPRs; its LDS records fit 6 blocks) beat 5 and natural.
 #ifndef IPT_MIN_BLOCKS_FWD
-#define IPT_MIN_BLOCKS_FWD 5
+#define IPT_MIN_BLOCKS_FWD 6
 #endif
 #ifndef IPT_MIN_BLOCKS_ADJ
-#define IPT_MIN_BLOCKS_ADJ 0
+#define IPT_MIN_BLOCKS_ADJ 6
 #endif
 #ifndef IPT_MIN_BLOCKS_GRAPH
 #define IPT_MIN_BLOCKS_GRAPH 0
@@ -384,6 +389,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     // ================= phase 2: next-event shadow ray (path_trace.cu:73-88)
     PHASE(2)
     V3 lo = mk(0.f, 0.f, 0.f);
+    float emit_s = 0.f;  // ADJ record: lo = Ke[emit_et] * emit_s
+    int emit_et = 0;
     if (__ballot(shadow)) {
       float ts = 0.f;
       int hs = -1;
@@ -415,6 +422,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             const float s = (float)(((double)(ct * ctp) / (td * td)) / (double)emit_pmf[emitter]);
 #endif
             lo = mk(me.ke[0] * s, me.ke[1] * s, me.ke[2] * s);
+            emit_s = s;
+            emit_et = et;
             const TriMat &m = mat[tri];
             if (SPEC && (m.flags & MAT_HAS_KS)) specd = phong(m.shininess, nh, din, sd);
             const float *kdt = kd_t + 3 * tri;
@@ -434,13 +443,13 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       if (MODE == MODE_ADJ) {  // vertex record k (layout [field][vertex][lane])
         float *rec = lds_rec + (size_t)k * kBlock + tid;
         const size_t fs = (size_t)vmax * kBlock;
-        rec[0] = __int_as_float(tri);
-        rec[fs] = lo.x;
-        rec[2 * fs] = lo.y;
-        rec[3 * fs] = lo.z;
-        rec[4 * fs] = specd;
-        rec[5 * fs] = coeff;
-        rec[6 * fs] = speci;
+        rec[0] = __uint_as_float((uint32_t)tri | ((uint32_t)emit_et << 16));
+        rec[fs] = emit_s;
+        rec[2 * fs] = coeff;
+        if (SPEC) {
+          rec[3 * fs] = specd;
+          rec[4 * fs] = speci;
+        }
       }
       if (MODE == MODE_GRAPH) {
         if (cont) {
@@ -486,6 +495,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           const float az = adj[pixel * 3 + 2] / (float)a.spp;
           V3 S = mk(0.f, 0.f, 0.f);
           // T_j = kd/pi (+ Ks*speci), D_j = kd (+ Ks*specd): exactly the forward's values
+          auto rec_lo = [&](int et, float es) {  // the forward's lo, same products
+            const TriMat &me = mat[et];
+            return mk(me.ke[0] * es, me.ke[1] * es, me.ke[2] * es);
+          };
           auto tdiff = [&](int tj, float si, float &x, float &y, float &z) {
             if (a.kd_tables) {
               const float *kp = kdpi_t + 3 * tj;
@@ -510,23 +523,26 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           if (escaped) {
             const float *r = lds_rec + (size_t)(K - 1) * kBlock + tid;
             float dx, dy, dz;
-            ddir(__float_as_int(r[0]), r[4 * fs], dx, dy, dz);
-            S = mk(Le.x + dx * r[fs], Le.y + dy * r[2 * fs], Le.z + dz * r[3 * fs]);
+            const uint32_t f0 = __float_as_uint(r[0]);
+            const V3 lk = rec_lo((int)(f0 >> 16), r[fs]);
+            ddir((int)(f0 & 0xffffu), SPEC ? r[3 * fs] : 0.f, dx, dy, dz);
+            S = mk(Le.x + dx * lk.x, Le.y + dy * lk.y, Le.z + dz * lk.z);
           }
           for (int kk = K - 1; kk >= 0; --kk) {
             // prefix throughput M_kk (recomputed exactly as the forward did)
             V3 Mk = mk(1.f, 1.f, 1.f);
             for (int j = 0; j < kk; ++j) {
               const float *rj = lds_rec + (size_t)j * kBlock + tid;
-              const float cj = rj[5 * fs];
+              const float cj = rj[2 * fs];
               float tx, ty, tz;
-              tdiff(__float_as_int(rj[0]), rj[6 * fs], tx, ty, tz);
+              tdiff((int)(__float_as_uint(rj[0]) & 0xffffu), SPEC ? rj[4 * fs] : 0.f, tx, ty, tz);
               Mk = mk((Mk.x * tx) * cj, (Mk.y * ty) * cj, (Mk.z * tz) * cj);
             }
             const float *r = lds_rec + (size_t)kk * kBlock + tid;
-            const int tk = __float_as_int(r[0]);
-            const V3 lk = mk(r[fs], r[2 * fs], r[3 * fs]);
-            const float sdk = r[4 * fs], ck = r[5 * fs], si = r[6 * fs];
+            const uint32_t f0 = __float_as_uint(r[0]);
+            const int tk = (int)(f0 & 0xffffu);
+            const V3 lk = rec_lo((int)(f0 >> 16), r[fs]);
+            const float ck = r[2 * fs], sdk = SPEC ? r[3 * fs] : 0.f, si = SPEC ? r[4 * fs] : 0.f;
             const bool last_esc = escaped && kk == K - 1;
             const bool continued = (kk < K - 1) || escaped;
             V3 dLd = Mk;
@@ -870,9 +886,14 @@ int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const f
     gpu_set_error("adjoint requires 0 <= max_bounces <= 62 (vertex records live in LDS)");
     return -1;
   }
+  if (s->host.nT > kMaxAdjTris) {
+    gpu_set_error("adjoint supports at most 65535 triangles");
+    return -1;
+  }
   const TraceArgs a = make_args(s, p);
   const size_t lds = (size_t)s->host.nT * 3 * sizeof(double) + table_bytes(a) +
-                     (size_t)(p.max_bounces + 1) * kRecFields * kBlock * sizeof(float);
+                     (size_t)(p.max_bounces + 1) * (s->has_ks ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock *
+                         sizeof(float);
   if (lds > 160 * 1024) {
     gpu_set_error("adjoint LDS footprint exceeds 160 KiB; lower max_bounces");
     return -1;
