@@ -197,7 +197,8 @@ __device__ __forceinline__ float dot3(V3 a, V3 b) { return fmaf(a.z, b.z, fmaf(a
 __device__ __forceinline__ V3 cross3(V3 a, V3 b) {
   return mk(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
 }
-__device__ __forceinline__ V3 unit(V3 v) {
+// Eigen's normalize with IEEE sqrtf and divisions (the definition).
+__device__ __forceinline__ V3 unit_ieee(V3 v) {
   const float n2 = dot3(v, v);
   if (n2 > 0.f) {
     const float s = sqrtf(n2);
@@ -236,6 +237,66 @@ __device__ __forceinline__ float div_inrange(float a, float b) {
   return a / b;
 #endif
 }
+
+// ---- in-range cores of the IEEE sqrt / division lowerings
+// hipcc lowers sqrtf to v_sqrt_f32 plus a one-ulp correction, wrapped in a
+// rescale for x < 2^-96 and a class test for +-0/+inf; sqrt (f64) to v_rsq_f64
+// plus Goldschmidt/Newton steps, wrapped in a rescale for x < 2^-767 and the
+// same class test.  Inside those ranges the wrappers are the identity, so the
+// cores below (the same instructions, same operands) ARE the IEEE results.
+__device__ __forceinline__ float sqrt_core(float x) {  // x in [2^-96, FLT_MAX]
+  float s = __builtin_amdgcn_sqrtf(x);
+  const float sm = __uint_as_float(__float_as_uint(s) - 1u);
+  const float sp = __uint_as_float(__float_as_uint(s) + 1u);
+  const float rm = fmaf(-sm, s, x);
+  const float rp = fmaf(-sp, s, x);
+  s = (0.f >= rm) ? sm : s;
+  s = (0.f < rp) ? sp : s;
+  return s;
+}
+__device__ __forceinline__ double dsqrt_core(double x) {  // x in [2^-767, DBL_MAX]
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = y * 0.5;
+  const double r = fma(-h, g, 0.5);
+  g = fma(g, r, g);
+  h = fma(h, r, h);
+  double d = fma(-g, g, x);
+  g = fma(d, h, g);
+  d = fma(-g, g, x);
+  g = fma(d, h, g);
+  return g;
+}
+// v / s for three numerators sharing the divisor's reciprocal refinement
+// (div_inrange with the r0/e0/r1 steps computed once).
+__device__ __forceinline__ V3 div3_core(V3 v, float s) {
+  const float ns = -s;
+  const float r0 = __builtin_amdgcn_rcpf(s);
+  const float e0 = fmaf(ns, r0, 1.0f);
+  const float r1 = fmaf(e0, r0, r0);
+  auto one = [&](float a) {
+    const float q0 = a * r1;
+    const float e1 = fmaf(ns, q0, a);
+    const float q1 = fmaf(e1, r1, q0);
+    const float e2 = fmaf(ns, q1, a);
+    return fmaf(e2, r1, q1);
+  };
+  return mk(one(v.x), one(v.y), one(v.z));
+}
+// unit_ieee(v) exactly.  Fast path when n2 in [2^-6, 2^60] (sqrt core valid;
+// s in [2^-3, 2^30]) and every component is 0 or >= 2^-90 in magnitude (so
+// each quotient is normal and no division would be rescaled): checked on the
+// bit patterns, (|bits| << 1) - 1 >= (bits(2^-90) << 1) - 1, with 0 wrapping
+// to the top.  Anything else takes the IEEE operations.
+__device__ __forceinline__ V3 unit(V3 v) {
+  const float n2 = dot3(v, v);
+  const uint32_t kLo = (0x25u << 24) - 1u;  // (bits(2^-90) << 1) - 1 = 0x24ffffff
+  const uint32_t m = min(min((__float_as_uint(v.x) << 1) - 1u, (__float_as_uint(v.y) << 1) - 1u),
+                         (__float_as_uint(v.z) << 1) - 1u);
+  if (n2 >= 0x1p-6f && n2 <= 0x1p60f && m >= kLo) return div3_core(v, sqrt_core(n2));
+  return unit_ieee(v);
+}
+// unit() for operands proven in range by construction (no test).
+__device__ __forceinline__ V3 unit_in_range(V3 v) { return div3_core(v, sqrt_core(dot3(v, v))); }
 
 // ------------------------------------------------------------ closest hit
 // Object::getIntersection (scene_basics.h:426-459) over every triangle in
@@ -367,7 +428,10 @@ __device__ __forceinline__ int closest_hit_pairs_small(const TriPair *__restrict
                                                        V3 p, V3 d, float &best_t) {
   float bt = __builtin_inff();
   int bi = -1;
-  const int nP = (nT + 1) >> 1;
+  // opaque copy: keeps the 16 per-pair guards as compare+branch here instead
+  // of being hoisted out of the megakernel loop as SGPR masks (which spill)
+  int nP = (nT + 1) >> 1;
+  asm volatile("" : "+s"(nP));
 #pragma unroll
   for (int j = 0; j < kSmallPairs; ++j) {
     if (j < nP) {  // wave-uniform
@@ -429,9 +493,12 @@ __device__ __forceinline__ V3 shading_normal(const TriGeom &g, V3 q) {
 __device__ __forceinline__ void camera_ray(const float *cam, Rng &st, int r, int c, int W, int H, V3 &p,
                                            V3 &d) {
   const float u0 = uniform(st), u1 = uniform(st);
-  const float x = 2.f * ((float)c + u0) / (float)W - 1.f;
-  const float y = 1.f - 2.f * ((float)r + u1) / (float)H;
-  const V3 d0 = unit(mk(x, y, 1.f));
+  // (2(c+u0)) / W: numerator in [2^-32, 2W], W >= 1 -- in div_inrange's range.
+  // d0 = (x, y, 1): x and y are 0 or multiples of 2^-24 (Sterbenz), n2 in
+  // [1, 3] -- in unit_in_range's range.
+  const float x = div_inrange(2.f * ((float)c + u0), (float)W) - 1.f;
+  const float y = 1.f - div_inrange(2.f * ((float)r + u1), (float)H);
+  const V3 d0 = unit_in_range(mk(x, y, 1.f));
   float pr[3], dr[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {

@@ -332,7 +332,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
 #ifdef IPT_ABL_DP  // timing-only ablation build
         const double sq = (double)sqrtf(r1);
 #else
-        const double sq = sqrt((double)r1);
+        const double sq = dsqrt_core((double)r1);  // r1 >= 2^-33: sqrt's identity range
 #endif
         const float ca = (float)(1.0 - sq);
         const float cb = (float)(sq * (double)(1.f - r2));
@@ -360,8 +360,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             cth = sqrtf(ut);
             sth = sqrtf(1.f - ut);
 #else
-            cth = sqrtf(ut);  // == (float)sqrt((double)ut): double rounding is innocuous for sqrt
-            sth = (float)sqrt(1.0 - (double)ut);
+            cth = sqrt_core(ut);  // == (float)sqrt((double)ut) (innocuous double rounding); ut >= 2^-33
+            const double omu = 1.0 - (double)ut;  // 0 or >= 2^-33
+            sth = omu > 0.0 ? (float)dsqrt_core(omu) : 0.f;
 #endif
             psamp = kInvPiF;
           } else {
