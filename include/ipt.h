@@ -73,6 +73,11 @@ const char *ipt_last_error(void);
 void ipt_clear_error(void);
 int ipt_abi_version(void);            /* 1 */
 int ipt_device_count(void);
+/* Diagnostic: bitwise self-test of the kernels' in-range sqrt/division cores
+ * against the IEEE operations over n random operands per test; counts[8]
+ * receives mismatch counts (0 expected; counts[6] is the number of unit()
+ * fast-path hits, not a mismatch).  No reference counterpart. */
+int ipt_selftest_math(uint64_t n, uint64_t seed, uint64_t *counts);
 
 /* Legacy-symbol configuration (defaults 500, 500, 100, -1, seed -1 = time). */
 void ipt_legacy_config(int width, int height, int spp, int max_bounces, int64_t seed);

@@ -65,6 +65,7 @@ SIGNATURES = {
     "ipt_clear_error": (None, []),
     "ipt_abi_version": (C.c_int, []),
     "ipt_device_count": (C.c_int, []),
+    "ipt_selftest_math": (C.c_int, [C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64)]),
     "ipt_legacy_config": (None, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int64]),
     "ipt_load_scene": (C.c_int, [C.c_int, fp, fp, fp, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.POINTER(vp)]),
     "ipt_load_scene_host": (C.c_int, [C.c_int, fp, fp, fp, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p),

@@ -45,6 +45,7 @@ int gpu_adjoint_host(GpuScene *s, const RenderParams &p, const float *adj, doubl
 int gpu_graph_host(GpuScene *s, const RenderParams &p, const uint8_t *target, double *acc);
 
 int gpu_device_count();
+int gpu_selftest_math(uint64_t n, uint64_t seed, uint64_t *counts);  // 8 mismatch counters
 const char *gpu_last_error();
 void gpu_set_error(const std::string &e);
 

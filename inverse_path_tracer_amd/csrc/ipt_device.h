@@ -218,7 +218,10 @@ __device__ __forceinline__ V3 along(V3 p, V3 d, float t) {
 // inputs.  In the hit test |b| = |n.d| lies in [1e-4, 1] and |a| <= scene
 // extent whenever the quotient is used (smaller |b| rejects the triangle
 // before t matters), so the scaling is the identity and the result equals
-// `a / b` bit for bit.  tests/test_gpu.py checks whole renders bit-exact.
+// `a / b` bit for bit -- except -0 / (b > 0), which gives +0 where IEEE
+// gives -0 (harmless at both call sites: the hit test rejects t = +-0 by
+// t < eps, the camera's numerator is positive).  Checked on the device by
+// ipt_selftest_math (tests/test_gpu.py).
 #ifndef IPT_FASTDIV
 #define IPT_FASTDIV 1
 #endif
@@ -266,8 +269,12 @@ __device__ __forceinline__ double dsqrt_core(double x) {  // x in [2^-767, DBL_M
   g = fma(d, h, g);
   return g;
 }
-// v / s for three numerators sharing the divisor's reciprocal refinement
-// (div_inrange with the r0/e0/r1 steps computed once).
+// v / s (s > 0) for three numerators sharing the divisor's reciprocal
+// refinement (div_inrange with the r0/e0/r1 steps computed once).  The
+// residuals are formed as -fma(s, q, -a): the same value as fma(-s, q, a) for
+// every nonzero residual (round-to-nearest is symmetric under negation), but
+// a -0 numerator then yields -0 as IEEE division does (fma(-s, -0, -0) would
+// give +0).  The negation folds into the next fma's input modifier.
 __device__ __forceinline__ V3 div3_core(V3 v, float s) {
   const float ns = -s;
   const float r0 = __builtin_amdgcn_rcpf(s);
@@ -275,9 +282,9 @@ __device__ __forceinline__ V3 div3_core(V3 v, float s) {
   const float r1 = fmaf(e0, r0, r0);
   auto one = [&](float a) {
     const float q0 = a * r1;
-    const float e1 = fmaf(ns, q0, a);
+    const float e1 = -fmaf(s, q0, -a);
     const float q1 = fmaf(e1, r1, q0);
-    const float e2 = fmaf(ns, q1, a);
+    const float e2 = -fmaf(s, q1, -a);
     return fmaf(e2, r1, q1);
   };
   return mk(one(v.x), one(v.y), one(v.z));

@@ -912,6 +912,114 @@ int gpu_graph(GpuScene *s, const RenderParams &p, const uint8_t *target_dev, dou
                             (hipStream_t)stream);
 }
 
+// ------------------------------------------------------------ math self-test
+// Diagnostic for the exactness claims behind the in-range cores: each core is
+// compared bitwise with the IEEE operation hipcc emits, over random operands
+// drawn across the whole range the core is used in (and the guard boundaries
+// of unit()).  counts[k] = mismatches of test k:
+//   0 sqrt_core vs sqrtf          x in [2^-96, 2^127]
+//   1 dsqrt_core vs sqrt (f64)    x in [2^-767, 2^1000]
+//   2 div_inrange vs a/b          |a| in [2^-100, 2^60], |b| in [2^-60, 2^60], |a/b| in [2^-120, 2^120]
+//   3 div_inrange, hit-test range |a| <= 2^20, |b| in [kMinDotUp, 1]
+//   4 div3_core vs v/s            unit()'s fast-path operands
+//   5 unit vs unit_ieee           vectors with zero / tiny / huge components (guard both ways)
+//   6 fast-path hits of test 5    (not a mismatch: shows both paths were exercised)
+//   7 camera division range       (2(c+u0))/W, c in [0, 2^16), W in [1, 2^16]
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ float rand_exp_float(uint64_t r, int emin, int emax) {  // sign random
+  const int e = emin + (int)((r >> 23) % (uint64_t)(emax - emin + 1));
+  const uint32_t m = (uint32_t)r & 0x7fffffu;
+  const uint32_t sgn = (uint32_t)(r >> 63) << 31;
+  return __uint_as_float(sgn | ((uint32_t)(e + 127) << 23) | m);
+}
+__global__ __launch_bounds__(kBlock) void math_selftest_kernel(uint64_t n, uint64_t seed,
+                                                               unsigned long long *counts) {
+  unsigned long long c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    const uint64_t r0 = mix64(seed ^ (i * 8 + 0)), r1 = mix64(seed ^ (i * 8 + 1)), r2 = mix64(seed ^ (i * 8 + 2));
+    const uint64_t r3 = mix64(seed ^ (i * 8 + 3)), r4 = mix64(seed ^ (i * 8 + 4));
+    {  // 0
+      const float x = fabsf(rand_exp_float(r0, -96, 127));
+      c[0] += __float_as_uint(sqrt_core(x)) != __float_as_uint(sqrtf(x));
+    }
+    {  // 1
+      const int e = -767 + (int)((r1 >> 52) % 1768u);
+      const double x = __longlong_as_double((long long)(((uint64_t)(e + 1023) << 52) | (r1 & 0xfffffffffffffull)));
+      c[1] += __double_as_longlong(dsqrt_core(x)) != __double_as_longlong(sqrt(x));
+    }
+    {  // 2
+      const float a = rand_exp_float(r2, -100, 60);  // nonzero: see div_inrange on zeros
+      const float b = rand_exp_float(r3, -60, 60);
+      const float q = a / b;
+      if (fabsf(q) >= 0x1p-120f && fabsf(q) <= 0x1p120f)
+        c[2] += __float_as_uint(div_inrange(a, b)) != __float_as_uint(q);
+    }
+    {  // 3
+      const float a = rand_exp_float(r4, -40, 20);
+      const float b = (r0 & 1 ? 1.f : -1.f) * (kMinDotUp + (1.f - kMinDotUp) * (float)(r3 >> 40) * 0x1p-24f);
+      c[3] += __float_as_uint(div_inrange(a, b)) != __float_as_uint(a / b);
+    }
+    {  // 4, 5, 6
+      V3 v;
+      float comp[3];
+      for (int k = 0; k < 3; ++k) {
+        const uint64_t rk = mix64(r4 ^ (uint64_t)(k + 11));
+        const int kind = (int)(rk & 15);
+        if (kind == 0) comp[k] = 0.f;
+        else if (kind == 1) comp[k] = (rk & 16) ? -0.f : 0.f;
+        else if (kind == 2) comp[k] = rand_exp_float(rk, -149 + 23, -85);   // tiny: around the 2^-90 guard
+        else if (kind == 3) comp[k] = rand_exp_float(rk, 25, 35);           // huge: around the 2^60 guard
+        else if (kind == 4) comp[k] = rand_exp_float(rk, -6, -2);           // small: around the 2^-6 guard
+        else comp[k] = rand_exp_float(rk, -30, 3);
+      }
+      v = mk(comp[0], comp[1], comp[2]);
+      const V3 u = unit(v), w = unit_ieee(v);
+      c[5] += (__float_as_uint(u.x) != __float_as_uint(w.x)) || (__float_as_uint(u.y) != __float_as_uint(w.y)) ||
+              (__float_as_uint(u.z) != __float_as_uint(w.z));
+      const float n2 = dot3(v, v);
+      const uint32_t m = min(min((__float_as_uint(v.x) << 1) - 1u, (__float_as_uint(v.y) << 1) - 1u),
+                             (__float_as_uint(v.z) << 1) - 1u);
+      const bool fast = n2 >= 0x1p-6f && n2 <= 0x1p60f && m >= ((0x25u << 24) - 1u);
+      c[6] += fast;
+      if (fast) {
+        const float sq = sqrtf(n2);
+        const V3 q = div3_core(v, sq);
+        c[4] += (__float_as_uint(q.x) != __float_as_uint(v.x / sq)) || (__float_as_uint(q.y) != __float_as_uint(v.y / sq)) ||
+                (__float_as_uint(q.z) != __float_as_uint(v.z / sq));
+      }
+    }
+    {  // 7
+      const int W = 1 + (int)(r0 % 65536u), cc = (int)(r1 % (uint64_t)W);
+      const float u0 = (float)(uint32_t)r2 * 2.3283064e-10f + 1.1641532e-10f;
+      const float a = 2.f * ((float)cc + u0);
+      c[7] += __float_as_uint(div_inrange(a, (float)W)) != __float_as_uint(a / (float)W);
+    }
+  }
+  for (int k = 0; k < 8; ++k)
+    if (c[k]) atomicAdd(&counts[k], c[k]);
+}
+
+int gpu_selftest_math(uint64_t n, uint64_t seed, uint64_t *counts_host) {
+  unsigned long long *d = nullptr;
+  HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d), 8 * sizeof(unsigned long long)));
+  int rc = 0;
+  if (hipMemset(d, 0, 8 * sizeof(unsigned long long)) != hipSuccess) rc = -1;
+  if (!rc) {
+    hipLaunchKernelGGL(math_selftest_kernel, dim3(2048), dim3(kBlock), 0, 0, n, seed, d);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = -1;
+  }
+  if (!rc && hipMemcpy(counts_host, d, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) rc = -1;
+  (void)hipFree(d);
+  if (rc) gpu_set_error("math self-test failed to run");
+  return rc;
+}
+
 // ------------------------------------------------------------ host wrappers
 namespace {
 struct DevBuf {

@@ -337,3 +337,19 @@ def test_material_recovery_c5_small():
         assert t.history[-1] < 0.5 * t.history[0]
         err = float((t.kd.detach() - t.truth)[18:][m].abs().mean())
         assert err < 0.5 * e0, (err, e0)
+
+
+def test_math_cores_bit_exact_on_device():
+    """The in-range sqrt/division cores used by the kernels equal the IEEE
+    operations bit for bit across their whole operand ranges (csrc
+    math_selftest_kernel: 2^24 random operand sets per test)."""
+    from inverse_path_tracer_amd import _native as N
+
+    counts = (C.c_uint64 * 8)()
+    N.check(N.lib().ipt_selftest_math(1 << 24, 12345, counts))
+    c = list(counts)
+    names = ["sqrt_core", "dsqrt_core", "div_inrange", "div_hit_range", "div3_core", "unit", "unit_fast_hits",
+             "div_camera"]
+    bad = {n: v for n, v in zip(names, c) if v and n != "unit_fast_hits"}
+    assert not bad, bad
+    assert 0.2 * (1 << 24) < c[6] < 0.95 * (1 << 24)  # both unit() paths exercised
