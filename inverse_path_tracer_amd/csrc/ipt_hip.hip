@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -56,7 +57,19 @@ constexpr int kBlock = 256;
 // Adjoint vertex record (per lane, in LDS): tri | et << 16, the emitter factor
 // s (lo = Ke[et] * s is rebuilt bit-identically in the sweep; s = 0 when the
 // shadow ray failed), coeff; with a Phong lobe also specd and speci.
-constexpr int kRecFieldsDiffuse = 3, kRecFieldsSpec = 5;
+// With IPT_ADJ_STORE_M the record also keeps the vertex's prefix throughput
+// M (the forward's own value), so the sweep is O(K) instead of recomputing
+// every prefix product (O(K^2)); costs 3 words per vertex of LDS, which drops
+// the adjoint from 6 to 5 blocks per CU at max_bounces = 4.  Measured
+// (profiles/r01_variants_adj_store_m.log): -3.4% on C2 (18 triangles), +4.4%
+// on C3 (30 triangles) -- off by default.
+#ifndef IPT_ADJ_STORE_M
+#define IPT_ADJ_STORE_M 0
+#endif
+constexpr int kRecM = 3;                                   // M.x at field 3 (if stored)
+constexpr int kRecSD = IPT_ADJ_STORE_M ? 6 : 3;            // specd, then speci
+constexpr int kRecFieldsDiffuse = IPT_ADJ_STORE_M ? 6 : 3;
+constexpr int kRecFieldsSpec = kRecFieldsDiffuse + 2;
 constexpr int kMaxAdjTris = 65535;  // tri and et share one 32-bit field
 constexpr int kEdgeW = 8;      // graph bin: w, w*f, pix[3]*w*f, light[3]*w*f
 constexpr int kMaxAdjBounces = 62;
@@ -447,9 +460,14 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         rec[0] = __uint_as_float((uint32_t)tri | ((uint32_t)emit_et << 16));
         rec[fs] = emit_s;
         rec[2 * fs] = coeff;
+        if (IPT_ADJ_STORE_M) {  // M_k: the throughput before this vertex's update
+          rec[kRecM * fs] = M.x;
+          rec[(kRecM + 1) * fs] = M.y;
+          rec[(kRecM + 2) * fs] = M.z;
+        }
         if (SPEC) {
-          rec[3 * fs] = specd;
-          rec[4 * fs] = speci;
+          rec[kRecSD * fs] = specd;
+          rec[(kRecSD + 1) * fs] = speci;
         }
       }
       if (MODE == MODE_GRAPH) {
@@ -526,24 +544,29 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             float dx, dy, dz;
             const uint32_t f0 = __float_as_uint(r[0]);
             const V3 lk = rec_lo((int)(f0 >> 16), r[fs]);
-            ddir((int)(f0 & 0xffffu), SPEC ? r[3 * fs] : 0.f, dx, dy, dz);
+            ddir((int)(f0 & 0xffffu), SPEC ? r[kRecSD * fs] : 0.f, dx, dy, dz);
             S = mk(Le.x + dx * lk.x, Le.y + dy * lk.y, Le.z + dz * lk.z);
           }
           for (int kk = K - 1; kk >= 0; --kk) {
-            // prefix throughput M_kk (recomputed exactly as the forward did)
-            V3 Mk = mk(1.f, 1.f, 1.f);
-            for (int j = 0; j < kk; ++j) {
-              const float *rj = lds_rec + (size_t)j * kBlock + tid;
-              const float cj = rj[2 * fs];
-              float tx, ty, tz;
-              tdiff((int)(__float_as_uint(rj[0]) & 0xffffu), SPEC ? rj[4 * fs] : 0.f, tx, ty, tz);
-              Mk = mk((Mk.x * tx) * cj, (Mk.y * ty) * cj, (Mk.z * tz) * cj);
-            }
+            // prefix throughput M_kk: recorded by the forward, or recomputed
+            // with exactly the forward's operations
             const float *r = lds_rec + (size_t)kk * kBlock + tid;
+            V3 Mk = mk(1.f, 1.f, 1.f);
+            if (IPT_ADJ_STORE_M) {
+              Mk = mk(r[kRecM * fs], r[(kRecM + 1) * fs], r[(kRecM + 2) * fs]);
+            } else {
+              for (int j = 0; j < kk; ++j) {
+                const float *rj = lds_rec + (size_t)j * kBlock + tid;
+                const float cj = rj[2 * fs];
+                float tx, ty, tz;
+                tdiff((int)(__float_as_uint(rj[0]) & 0xffffu), SPEC ? rj[(kRecSD + 1) * fs] : 0.f, tx, ty, tz);
+                Mk = mk((Mk.x * tx) * cj, (Mk.y * ty) * cj, (Mk.z * tz) * cj);
+              }
+            }
             const uint32_t f0 = __float_as_uint(r[0]);
             const int tk = (int)(f0 & 0xffffu);
             const V3 lk = rec_lo((int)(f0 >> 16), r[fs]);
-            const float ck = r[2 * fs], sdk = SPEC ? r[3 * fs] : 0.f, si = SPEC ? r[4 * fs] : 0.f;
+            const float ck = r[2 * fs], sdk = SPEC ? r[kRecSD * fs] : 0.f, si = SPEC ? r[(kRecSD + 1) * fs] : 0.f;
             const bool last_esc = escaped && kk == K - 1;
             const bool continued = (kk < K - 1) || escaped;
             V3 dLd = Mk;
@@ -766,6 +789,9 @@ static int resident_grid(GpuScene *s, size_t lds_bytes, int *grid) {
     }
     s->grid[slot] = per_cu * cus;
     s->grid_lds[slot] = lds_bytes;
+    if (std::getenv("IPT_DEBUG_GRID"))
+      std::fprintf(stderr, "[ipt] trace_kernel<%d,%d>: %zu B LDS/block, %d blocks/CU x %d CUs\n", MODE, (int)SPEC,
+                   lds_bytes, per_cu, cus);
   }
   *grid = s->grid[slot];
   return 0;
