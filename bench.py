@@ -55,36 +55,50 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(target_seconds=12.0):
-    """The CPU oracle (test infrastructure) on a bounded row band of the same
-    frame, all of this rank's allowed cores (capped at 16)."""
+def cpu_baseline(fwd_seconds=8.0, one_core_seconds=3.0, adj_seconds=4.0):
+    """The CPU oracle (test infrastructure, oracle/ipt_oracle.c -O2 OpenMP) on
+    bounded samples of the same C2 workload: whole frames (consecutive frame
+    seeds) on this rank's allowed cores (capped at 16) until fwd_seconds, the
+    first rows on ONE core, and the adjoint on the first rows."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
 
     cores = min(16, len(os.sched_getaffinity(0)))
     L = oracle_lib.lib()
-    L.oro_set_threads(cores)
     recs = [(o.pos, o.ori, o.scl, o.obj_file, o.mtl_file) for o in CORNELL]
     sc = oracle_lib.OracleScene(recs)
-    rows, done, secs = 4, 0, 0.0
-    while secs < target_seconds and done < H:
-        r = min(rows, H - done)
+
+    def rows_for(seconds, fn):
+        rows, done, secs = 4, 0, 0.0
+        while secs < seconds and done < H:
+            r = min(rows, H - done)
+            t0 = time.perf_counter()
+            fn(done, done + r)
+            secs += time.perf_counter() - t0
+            done += r
+            rows *= 2
+        return done, secs
+
+    L.oro_set_threads(cores)
+    frames, secs = 0, 0.0
+    while secs < fwd_seconds and frames < 16:
         t0 = time.perf_counter()
-        sc.render_samples(W, H, SPP, BOUNCES, 0, done * W * SPP, (done + r) * W * SPP)
+        sc.render_samples(W, H, SPP, BOUNCES, frame_seed(0, frames, W, H, SPP))
         secs += time.perf_counter() - t0
-        done += r
-        rows *= 2
-    fwd = done * W * SPP / secs / 1e6
-    # adjoint on a smaller band
-    grows = max(1, min(H, int(done // 4)))
+        frames += 1
+    fwd = frames * W * H * SPP / secs / 1e6
     adj = np.ones((H, W, 3), np.float32)
-    t0 = time.perf_counter()
-    sc.adjoint(W, H, SPP, BOUNCES, 0, adj, 0, grows)
-    gsecs = time.perf_counter() - t0
+    arows, asecs = rows_for(adj_seconds, lambda b, e: sc.adjoint(W, H, SPP, BOUNCES, 0, adj, b, e))
+    L.oro_set_threads(1)
+    orows, osecs = rows_for(one_core_seconds,
+                            lambda b, e: sc.render_samples(W, H, SPP, BOUNCES, 0, b * W * SPP, e * W * SPP))
+    L.oro_set_threads(cores)
     return {"value": round(fwd, 3), "unit": "Msamples/s", "cores": cores, "kind": "port",
-            "sample": "CPU oracle (oracle/ipt_oracle.c, -O2 OpenMP) on rows [0,%d) of the C2 frame "
-                      "(%d samples, %.1f s); adjoint on rows [0,%d)" % (done, done * W * SPP, secs, grows),
-            "grad_value": round(grows * W * SPP / gsecs / 1e6, 3)}
+            "sample": "CPU oracle (oracle/ipt_oracle.c, -O2 OpenMP) on %d whole C2 frame(s) (%d samples, %.1f s); "
+                      "adjoint on rows [0,%d) (%.1f s); 1 core on rows [0,%d) (%.1f s)" % (
+                          frames, frames * W * H * SPP, secs, arows, asecs, orows, osecs),
+            "grad_value": round(arows * W * SPP / asecs / 1e6, 3),
+            "value_1core": round(orows * W * SPP / osecs / 1e6, 3)}
 
 
 def main():
@@ -173,6 +187,14 @@ def main():
     if os.path.exists(PMC_FILE):
         with open(PMC_FILE) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
+    # SURVEY.md §8(d) "HBM fraction": PMC-measured bytes of the same kernel
+    # (profiles/, FETCH x2 + WRITE) over this run's kernel time, vs 8 TB/s
+    hbm = None
+    if traffic:
+        gbs = traffic / (kernel_ms / 1e3) / 1e9
+        hbm = {"bytes_per_launch": traffic, "achieved_GBps": round(gbs, 1), "peak_GBps": 8000.0,
+               "frac": round(gbs / 8000.0, 4), "algorithmic_bytes_per_launch": samples_per_frame * 12,
+               "source": os.path.relpath(PMC_FILE, ROOT)}
     roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
                 "kernel": "trace_kernel<MODE_FWD>", "kernel_ms": round(kernel_ms, 4),
@@ -195,7 +217,7 @@ def main():
             "grad_value": round(grad_value, 2), "grad_unit": "grad-Msamples/s",
             "grad_ms_per_step": round(bwd_ms / args.steps, 4),
             "wall_s_fwd_region": round(wall_fwd, 4),
-            "roofline": roofline, "cpu_baseline": cpu,
+            "roofline": roofline, "hbm": hbm, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

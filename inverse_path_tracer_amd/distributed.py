@@ -11,6 +11,9 @@ single-GPU result bit-for-bit (forward) or up to fp64 summation order
   rank wants the whole image); the adjoint's only exchange is ONE all-reduce
   of the nT*3 fp64 gradient (``allreduce_``), 720 B for 30 triangles --
   latency-bound on xGMI, no bucketing needed.
+* createGraph (G3) across ranks (``graph_sharded``): per-rank row-band fp64
+  bins, ONE all-reduce of the (nT+1)*nT*8 bins (59.5 KB for nT = 30), then
+  DataWrapper::compress on every rank.
 * Weak scaling (bench.py): every rank renders its own frame of the same
   configuration; frame f uses the seed offset ``frame_seed`` so the global
   sample index space stays disjoint across frames.
@@ -58,3 +61,24 @@ def gather_rows(band: torch.Tensor, height: int) -> torch.Tensor:
     out = [torch.empty_like(pad) for _ in range(W)]
     dist.all_gather(out, pad)
     return torch.cat([o[: e - b] for o, (b, e) in zip(out, bands)], dim=0)
+
+
+def graph_sharded(scene, target, width: int, height: int, spp: int, max_bounces=None, seed: int = 0,
+                  device=None):
+    """createGraph (inv_path_trace.cu:195-208) sharded by row bands: returns the
+    compressed (nT+1)*nT*7 floats, identical on every rank and equal to the
+    single-GPU result up to fp64 summation order.  `scene` is a Scene (or any
+    object with .nT and .graph(target, W, H, spp, mb, seed, row_begin, row_end)
+    returning (bins, data))."""
+    import numpy as np
+
+    from .scene import compress
+
+    W, R = world()
+    b, e = shard_rows(height, W, R)
+    bins, _ = scene.graph(target, width, height, spp, max_bounces, seed, b, e)
+    t = torch.from_numpy(np.ascontiguousarray(bins, np.float64))
+    if device is not None:
+        t = t.to(device)
+    allreduce_(t)
+    return compress(scene.nT, t.cpu().numpy())

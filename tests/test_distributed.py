@@ -45,8 +45,19 @@ def _worker(rank, world, port, out):
     s, _ = sc.render_samples(W, H, SPP, MB, SEED, b * W * SPP, e * W * SPP)
     hdr, _ = oracle_lib.pixel_mean(s, (e - b) * W, SPP)
     img = gather_rows(torch.from_numpy(hdr.reshape(e - b, W, 3)), H)
+    # createGraph: per-rank bins of the row band, one all-reduce, compress
+    from inverse_path_tracer_amd.distributed import graph_sharded
+
+    class _OracleGraph:  # the Scene.graph calling convention over the oracle
+        nT = sc.nT
+
+        def graph(self, target, w, h, spp, mb, seed, rb, re):
+            return sc.graph(w, h, spp, mb, seed, target, rb, re)
+
+    target = np.random.RandomState(3).randint(0, 256, (H, W, 3)).astype(np.uint8)
+    data = torch.from_numpy(graph_sharded(_OracleGraph(), target, W, H, SPP, MB, SEED))
     if rank == 0:
-        torch.save({"g": g, "img": img}, out)
+        torch.save({"g": g, "img": img, "graph": data}, out)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -64,3 +75,7 @@ def test_row_band_sharding_gloo(oracle, tmp_path, world):
     assert np.array_equal(res["img"].numpy().view(np.uint32), hdr_full.view(np.uint32))
     # gradient: equal up to fp64 summation order
     np.testing.assert_allclose(res["g"].numpy(), g_full, rtol=1e-12, atol=1e-15)
+    # graph: bins summed across ranks then compressed == the single-rank result
+    target = np.random.RandomState(3).randint(0, 256, (H, W, 3)).astype(np.uint8)
+    acc_full, data_full = sc.graph(W, H, SPP, MB, SEED, target)
+    np.testing.assert_allclose(res["graph"].numpy(), data_full, rtol=1e-6, atol=1e-7)

@@ -353,3 +353,13 @@ def test_math_cores_bit_exact_on_device():
     bad = {n: v for n, v in zip(names, c) if v and n != "unit_fast_hits"}
     assert not bad, bad
     assert 0.2 * (1 << 24) < c[6] < 0.95 * (1 << 24)  # both unit() paths exercised
+
+
+def test_c1_golden_vectors_on_device():
+    """BASELINE config C1 on the GPU equals the committed oracle golden vectors
+    bit for bit (HDR and tonemapped u8)."""
+    g = np.load(os.path.join(TESTS, "golden", "c1_cornell_128x128x8_b2_seed0.npz"))
+    P = product_scene(CORNELL)
+    hdr, u8 = P.render(128, 128, 8, 2, 0, ldr=True)
+    assert np.array_equal(bits(hdr), bits(g["hdr"]))
+    assert np.array_equal(u8, g["ldr"])

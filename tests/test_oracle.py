@@ -224,3 +224,20 @@ def test_graph_structure(oracle):
     w = data[: (nT + 1) * nT].reshape(nT + 1, nT)
     rows = w.sum(1)
     assert np.all((np.abs(rows - 1) < 1e-5) | (rows == 0))  # row-normalised log weights
+
+
+def test_c1_golden_vectors(oracle):
+    """The oracle reproduces the committed C1 golden vectors bit for bit
+    (tests/golden/make_c1_golden.py)."""
+    import os
+
+    import numpy as np
+    from conftest import CORNELL, TESTS
+
+    g = np.load(os.path.join(TESTS, "golden", "c1_cornell_128x128x8_b2_seed0.npz"))
+    sc = oracle.OracleScene(CORNELL)
+    s, casts = sc.render_samples(128, 128, 8, 2, 0)
+    hdr, ldr = oracle.pixel_mean(s, 128 * 128, 8)
+    assert int(casts) == int(g["casts"])
+    assert np.array_equal(hdr.reshape(128, 128, 3).view(np.uint32), g["hdr"].view(np.uint32))
+    assert np.array_equal(ldr.reshape(128, 128, 3), g["ldr"])
