@@ -363,3 +363,41 @@ def test_c1_golden_vectors_on_device():
     hdr, u8 = P.render(128, 128, 8, 2, 0, ldr=True)
     assert np.array_equal(bits(hdr), bits(g["hdr"]))
     assert np.array_equal(u8, g["ldr"])
+
+
+def _one_triangle_obj(tmp_path, name="tri.obj", z=0.0):
+    p = tmp_path / name
+    p.write_text("v -0.4 -0.3 %g\nv 0.5 -0.2 %g\nv 0.1 0.45 %g\nf 1 2 3\n" % (z, z + 0.1, z - 0.05))
+    return str(p)
+
+
+@pytest.mark.parametrize("extra_cubes", [0, 2])
+def test_odd_triangle_counts_bit_exact(oracle, tmp_path, extra_cubes):
+    """Odd nT exercises the zero-triangle padding of the last TriPair: nT = 19
+    (unrolled small-scene loop) and nT = 43 (generic pair loop, LDS tables)."""
+    recs = CORNELL + [((0.2, -0.6, 3.6), (0.3, 0.2, 0.1), (1, 1, 1), _one_triangle_obj(tmp_path), "*Kd 0.7 0.2 0.4*")]
+    for i in range(extra_cubes):
+        recs.append(((-0.5 + i, -1.5, 4.2 + 0.3 * i), (0, 0.4 * i, 0), (0.5, 0.5, 0.5), CUBE_OBJ, "*Kd 0.3 0.8 0.5*"))
+    P, Q = product_scene(recs), oracle.OracleScene(recs)
+    assert P.nT == 19 + 12 * extra_cubes and P.nT % 2 == 1
+    got = P.render_samples(40, 32, 6, 4, 21)
+    want, _ = Q.render_samples(40, 32, 6, 4, 21)
+    assert np.array_equal(bits(got), bits(want))
+    adj = np.random.RandomState(5).uniform(-1, 1, (32, 40, 3)).astype(np.float32)
+    np.testing.assert_allclose(P.adjoint(adj, 40, 32, 6, 4, 21), Q.adjoint(40, 32, 6, 4, 21, adj), rtol=1e-9,
+                               atol=1e-12)
+
+
+def test_large_scene_adjoint_and_graph(oracle):
+    """nT = 1298 (sphere): no LDS kd tables (nT > 512) in the adjoint sweep and
+    global-memory graph bins (> 64 KB)."""
+    recs = CORNELL + [((0.3, -1.2, 4.2), (0.0, 0.4, 0.0), (1.2, 1.2, 1.2), SPHERE_OBJ, "*Kd 0.2 0.6 0.3*")]
+    P, Q = product_scene(recs), oracle.OracleScene(recs)
+    W = H = 12
+    adj = np.random.RandomState(8).uniform(-1, 1, (H, W, 3)).astype(np.float32)
+    np.testing.assert_allclose(P.adjoint(adj, W, H, 3, 3, 4), Q.adjoint(W, H, 3, 3, 4, adj), rtol=1e-9, atol=1e-12)
+    tgt = np.random.RandomState(9).randint(0, 256, (H, W, 3)).astype(np.uint8)
+    acc, data = P.graph(tgt, W, H, 2, 3, 4)
+    acc_q, data_q = Q.graph(W, H, 2, 3, 4, tgt)
+    np.testing.assert_allclose(acc, acc_q, rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(data, data_q, rtol=1e-6, atol=1e-7)
