@@ -99,6 +99,32 @@ int ipt_scene_get_materials(void *scene, float *kd);
 int ipt_scene_set_materials(void *scene, const float *kd);
 int ipt_scene_camera(void *scene, float *out16);
 
+/* Acceleration structure for closest-hit queries.  The reference's BVH
+ * (bvh.h:109-205) is over objects and, for its <= 4-object scenes, one leaf:
+ * brute force over all triangles, ties to the lowest index
+ * (scene_basics.h:426-459, bvh.h:55-77).  Here scenes of >= 64 triangles
+ * trace a triangle BVH that returns exactly the same hits;
+ * AUTO picks it, BRUTE/BVH force either (BVH fails if the scene has none). */
+#define IPT_ACCEL_AUTO 0
+#define IPT_ACCEL_BRUTE 1
+#define IPT_ACCEL_BVH 2
+int ipt_scene_set_accel(void *scene, int mode);
+/* info4 = {nodes, leaf pairs, depth, accel in use (IPT_ACCEL_BRUTE/BVH)};
+ * returns 1 if the scene has a BVH, 0 if not (ipt_last_error says why). */
+int ipt_scene_bvh_info(void *scene, int32_t *info4);
+/* nodes: info4[0]*16 floats (BvhNode), pairs: info4[1]*40 floats (BvhPair:
+ * 18 field pairs, then 2 int32 triangle indices, 2 pad); either nullable. */
+int ipt_scene_export_bvh(void *scene, float *nodes, float *pairs);
+/* Closest hit of n rays (origins, dirs: n*3 floats) through the kernels'
+ * own cast: idx = triangle index or -1, t = its distance.  targets
+ * (nullable, n ints): >= 0 marks a next-event shadow ray towards that
+ * emitter triangle, for which only "idx == target" and then t are defined
+ * (the BVH stops once the target is known to be occluded). */
+int ipt_closest_hit_host(void *scene, int64_t n, const float *origins, const float *dirs, const int32_t *targets,
+                         float *t, int32_t *idx);
+int ipt_closest_hit_dev(void *scene, int64_t n, const float *origins_dev, const float *dirs_dev,
+                        const int32_t *targets_dev, float *t_dev, int32_t *idx_dev, void *stream);
+
 /* Host-memory entry points (synchronous). */
 int ipt_render_samples_host(void *scene, const ipt_params_t *p, float *samples); /* rows*W*spp*3 */
 int ipt_render_host(void *scene, const ipt_params_t *p, float *hdr, uint8_t *ldr); /* rows*W*3 */

@@ -17,6 +17,8 @@ LIB_PATH = os.environ.get("IPT_AMD_LIB") or os.path.join(_HERE, "lib", "libipt_a
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ipt.h")
 TRI_EXPORT_STRIDE = 57
 ACC_WIDTH = 8
+# acceleration modes (include/ipt.h IPT_ACCEL_*)
+ACCEL_AUTO, ACCEL_BRUTE, ACCEL_BVH = 0, 1, 2
 
 
 class NativeError(RuntimeError):
@@ -88,6 +90,11 @@ SIGNATURES = {
     "ipt_pixel_mean_sm_dev": (C.c_int, [vp, C.c_int64, C.c_int, vp, vp, vp]),
     "ipt_adjoint_dev": (C.c_int, [vp, pp, vp, vp, vp, vp]),
     "ipt_graph_dev": (C.c_int, [vp, pp, vp, vp, vp]),
+    "ipt_scene_set_accel": (C.c_int, [vp, C.c_int]),
+    "ipt_scene_bvh_info": (C.c_int, [vp, C.POINTER(C.c_int32)]),
+    "ipt_scene_export_bvh": (C.c_int, [vp, fp, fp]),
+    "ipt_closest_hit_host": (C.c_int, [vp, C.c_int64, fp, fp, C.POINTER(C.c_int32), fp, C.POINTER(C.c_int32)]),
+    "ipt_closest_hit_dev": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp, vp, vp]),
     "ipt_png_write": (C.c_int, [C.c_char_p, C.c_int, C.c_int, u8p]),
     "ipt_png_read": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), u8p, C.c_int64]),
 }

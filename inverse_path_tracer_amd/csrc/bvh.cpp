@@ -1,0 +1,370 @@
+// bvh.cpp -- triangle BVH for the exact closest-hit traversal.
+//
+// What "exact" needs.  The reference's closest hit is the
+// brute-force loop of Object::getIntersection (scene_basics.h:426-459) over
+// every triangle in order with a strict `<`, i.e. the lexicographic minimum
+// of (t, triangle index) over the triangles whose fp32 test accepts.  A BVH
+// returns the same hit iff it never prunes a triangle that the fp32 test
+// would accept with (t, i) below the current best.  Three facts make that so:
+//
+//  1. Acceptance region.  The test accepts a hit point q only if its three
+//     computed edge-plane distances are <= 0 and q came from the plane
+//     equation.  With unit rounding u = 2^-24 the computed distance of a
+//     3-term fma chain is within ds = 2^-21 (|e3| + 3 Q) of the exact
+//     distance (Q bounds |q|), and q lies within h = 2^-17 * 3 R of the
+//     triangle's plane (R bounds every ray origin and hit point: the scene's
+//     coordinates and the camera).  So q lies in the prism of the three
+//     relaxed half-spaces e_k.x + e3_k <= ds_k cut by the slab
+//     |n.(x - c)| <= h: a convex solid whose six vertices are solved below in
+//     double precision (Cramer's rule).  A triangle whose relaxed region is
+//     not bounded (edge planes not forming a triangle, non-finite fields)
+//     makes the whole scene fall back to the brute-force loop.
+//  2. Slab test.  The traversal computes each slab parameter as
+//     fma(lo, 1/d, -p/d): the exact crossing parameter of a plane displaced
+//     by at most 2u(|lo| + 2|p|) <= 6uR.  Boxes are padded by 2^-16 R (over
+//     40x that, plus the u|q| between the rounded hit point and the exact ray
+//     point), so the computed [entry, exit] always contains the parameter of
+//     every acceptable hit.  Slabs with |d| < 2^-60 are dropped (NaN, ignored
+//     by min/max): conservative.
+//  3. Order.  The leaf test keeps (t, index) lexicographically; a box is
+//     pruned only when its entry parameter exceeds the current best t.
+//
+// The build is a binned SAH (32 bins, pair-granular leaf cost) over the
+// acceptance boxes; nodes are emitted breadth-first, leaves as field-
+// interleaved triangle pairs in depth-first leaf order.
+#include "bvh.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+
+namespace ipt {
+
+namespace {
+
+constexpr int kBins = 32;
+constexpr int kMaxLeafTris = 8;  // SAH may stop at <= 8 triangles (4 pairs)
+constexpr double kCostNode = 1.0, kCostPair = 1.0;
+
+struct Box {
+  float lo[3] = {std::numeric_limits<float>::infinity(), std::numeric_limits<float>::infinity(),
+                 std::numeric_limits<float>::infinity()};
+  float hi[3] = {-std::numeric_limits<float>::infinity(), -std::numeric_limits<float>::infinity(),
+                 -std::numeric_limits<float>::infinity()};
+  void grow(const Box &b) {
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = std::min(lo[a], b.lo[a]);
+      hi[a] = std::max(hi[a], b.hi[a]);
+    }
+  }
+  void grow(const float *p) {
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = std::min(lo[a], p[a]);
+      hi[a] = std::max(hi[a], p[a]);
+    }
+  }
+  double area() const {
+    if (!(hi[0] >= lo[0])) return 0.0;
+    const double dx = (double)hi[0] - lo[0], dy = (double)hi[1] - lo[1], dz = (double)hi[2] - lo[2];
+    return 2.0 * (dx * dy + dy * dz + dz * dx);
+  }
+};
+
+struct Prim {
+  Box box;
+  float c[3];
+  int tri;
+};
+
+struct TNode {  // build-time inner node
+  Box box[2];
+  int kid[2];   // >= 0 inner (build index); < 0: ~leaf id
+};
+
+struct Builder {
+  std::vector<Prim> prims;
+  std::vector<TNode> nodes;
+  std::vector<std::pair<int, int>> leaves;  // [begin, end) into prims
+  int max_depth = 0;
+  bool too_deep = false;
+
+  static int pairs_of(int n) { return (n + 1) / 2; }
+
+  // Returns the child code for prims[b, e) and its box.
+  int build(int b, int e, int depth, bool force_split, Box *out_box) {
+    Box box, cbox;
+    for (int i = b; i < e; ++i) {
+      box.grow(prims[i].box);
+      cbox.grow(prims[i].c);
+    }
+    *out_box = box;
+    const int n = e - b;
+    const double leaf_cost = kCostPair * pairs_of(n);
+    const bool can_leaf = pairs_of(n) <= (1 << kBvhLeafPairBits);
+    if (!force_split && n <= 2) return make_leaf(b, e);
+    if (depth >= kBvhMaxDepth - 1) {
+      if (can_leaf) return make_leaf(b, e);
+      too_deep = true;
+      return make_leaf(b, b + 1);  // build is discarded
+    }
+    // binned SAH over centroids
+    int best_axis = -1, best_split = -1;
+    double best_cost = std::numeric_limits<double>::infinity();
+    const double parent_area = std::max(box.area(), 1e-30);
+    for (int a = 0; a < 3; ++a) {
+      const double lo = cbox.lo[a], ext = (double)cbox.hi[a] - lo;
+      if (!(ext > 0.0)) continue;
+      Box bb[kBins];
+      int cnt[kBins] = {0};
+      for (int i = b; i < e; ++i) {
+        int k = (int)((prims[i].c[a] - lo) / ext * kBins);
+        k = std::min(std::max(k, 0), kBins - 1);
+        cnt[k]++;
+        bb[k].grow(prims[i].box);
+      }
+      double right_area[kBins];
+      int right_cnt[kBins];
+      Box acc;
+      int ac = 0;
+      for (int k = kBins - 1; k > 0; --k) {
+        acc.grow(bb[k]);
+        ac += cnt[k];
+        right_area[k] = acc.area();
+        right_cnt[k] = ac;
+      }
+      Box lacc;
+      int lc = 0;
+      for (int k = 1; k < kBins; ++k) {
+        lacc.grow(bb[k - 1]);
+        lc += cnt[k - 1];
+        if (lc == 0 || right_cnt[k] == 0) continue;
+        const double cost = kCostNode + (lacc.area() * kCostPair * pairs_of(lc) +
+                                         right_area[k] * kCostPair * pairs_of(right_cnt[k])) / parent_area;
+        if (cost < best_cost) {
+          best_cost = cost;
+          best_axis = a;
+          best_split = k;
+        }
+      }
+    }
+    if (!force_split && n <= kMaxLeafTris && leaf_cost <= best_cost) return make_leaf(b, e);
+    int mid;
+    if (best_axis >= 0) {
+      const int a = best_axis;
+      const double lo = cbox.lo[a], ext = (double)cbox.hi[a] - lo;
+      auto it = std::partition(prims.begin() + b, prims.begin() + e, [&](const Prim &p) {
+        int k = (int)((p.c[a] - lo) / ext * kBins);
+        k = std::min(std::max(k, 0), kBins - 1);
+        return k < best_split;
+      });
+      mid = (int)(it - prims.begin());
+    } else {
+      mid = b;  // all centroids equal
+    }
+    if (mid == b || mid == e) {  // degenerate: median by index along the widest axis
+      int a = 0;
+      for (int k = 1; k < 3; ++k)
+        if ((double)cbox.hi[k] - cbox.lo[k] > (double)cbox.hi[a] - cbox.lo[a]) a = k;
+      mid = b + n / 2;
+      std::nth_element(prims.begin() + b, prims.begin() + mid, prims.begin() + e, [&](const Prim &x, const Prim &y) {
+        return x.c[a] < y.c[a] || (x.c[a] == y.c[a] && x.tri < y.tri);
+      });
+    }
+    const int id = (int)nodes.size();
+    nodes.emplace_back();
+    max_depth = std::max(max_depth, depth + 1);
+    Box lb, rb;
+    const int l = build(b, mid, depth + 1, false, &lb);
+    const int r = build(mid, e, depth + 1, false, &rb);
+    nodes[id].box[0] = lb;
+    nodes[id].box[1] = rb;
+    nodes[id].kid[0] = l;
+    nodes[id].kid[1] = r;
+    return id;
+  }
+
+  int make_leaf(int b, int e) {
+    leaves.emplace_back(b, e);
+    return ~(int)(leaves.size() - 1);
+  }
+};
+
+void put_tri(BvhPair *P, int h, const TriIsect *T, int idx) {
+  float v[18] = {0.f};
+  if (T) {
+    const float src[18] = {T->c[0], T->c[1], T->c[2], T->n[0], T->n[1], T->n[2], T->e0[0], T->e0[1], T->e0[2],
+                           T->e0[3], T->e1[0], T->e1[1], T->e1[2], T->e1[3], T->e2[0], T->e2[1], T->e2[2], T->e2[3]};
+    std::memcpy(v, src, sizeof v);
+  }
+  for (int k = 0; k < 18; ++k) P->f[k][h] = v[k];
+  P->idx[h] = idx;
+}
+
+float round_down(double x) {
+  float f = (float)x;
+  if ((double)f > x) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
+  return f;
+}
+float round_up(double x) {
+  float f = (float)x;
+  if ((double)f < x) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+  return f;
+}
+
+}  // namespace
+
+double scene_coord_bound(const HostScene &S) {
+  double m = 0.0;
+  for (const TriGeom &g : S.geom)
+    for (int j = 0; j < 3; ++j)
+      for (int a = 0; a < 3; ++a) m = std::max(m, std::fabs((double)g.v[j][a]));
+  for (int a = 0; a < 3; ++a) m = std::max(m, std::fabs((double)S.cam[4 * a + 3]));  // camera origin M*(0,0,0,1)
+  return m + 1.0;
+}
+
+int acceptance_box(const TriIsect &T, const TriGeom &G, double r_all, float lo[3], float hi[3]) {
+  const float *fields[5] = {T.c, T.n, T.e0, T.e1, T.e2};
+  const int counts[5] = {3, 3, 4, 4, 4};
+  for (int f = 0; f < 5; ++f)
+    for (int k = 0; k < counts[f]; ++k)
+      if (!std::isfinite(fields[f][k])) return -1;
+  const double n[3] = {T.n[0], T.n[1], T.n[2]};
+  if (n[0] == 0.0 && n[1] == 0.0 && n[2] == 0.0) return 1;  // |n.d| = 0 < 1e-4 for every ray
+  double q = 0.0;
+  for (int j = 0; j < 3; ++j)
+    for (int a = 0; a < 3; ++a) q = std::max(q, std::fabs((double)G.v[j][a]));
+  q += 1.0;
+  const float *pl[3] = {T.e0, T.e1, T.e2};
+  double e[3][3], d[3], ds[3];
+  for (int k = 0; k < 3; ++k) {
+    for (int a = 0; a < 3; ++a) e[k][a] = pl[k][a];
+    d[k] = pl[k][3];
+    ds[k] = std::ldexp(std::fabs(d[k]) + 3.0 * q, -21);
+  }
+  const double h = std::ldexp(3.0 * r_all, -17);
+  const double nc = n[0] * T.c[0] + n[1] * T.c[1] + n[2] * T.c[2];
+  auto cross = [](const double *a, const double *b, double *o) {
+    o[0] = a[1] * b[2] - a[2] * b[1];
+    o[1] = a[2] * b[0] - a[0] * b[2];
+    o[2] = a[0] * b[1] - a[1] * b[0];
+  };
+  auto dot = [](const double *a, const double *b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; };
+  auto norm = [&](const double *a) { return std::sqrt(dot(a, a)); };
+  double blo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, bhi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+  for (int j = 0; j < 3; ++j) {
+    const int k = (j + 1) % 3, i = (j + 2) % 3;
+    double ejk[3], ekn[3], nej[3];
+    cross(e[j], e[k], ejk);
+    cross(e[k], n, ekn);
+    cross(n, e[j], nej);
+    const double det = dot(n, ejk);
+    if (!(std::fabs(det) > 1e-9 * norm(n) * norm(e[j]) * norm(e[k]))) return -1;
+    for (int s = -1; s <= 1; ++s) {
+      const double b0 = nc + s * h, b1 = ds[j] - d[j], b2 = ds[k] - d[k];
+      double x[3];
+      for (int a = 0; a < 3; ++a) x[a] = (b0 * ejk[a] + b1 * ekn[a] + b2 * nej[a]) / det;
+      if (s == 0) {  // bounded iff every vertex satisfies the third half-space
+        if (!(dot(e[i], x) + d[i] <= ds[i] * (1.0 + 1e-9))) return -1;
+      } else {
+        for (int a = 0; a < 3; ++a) {
+          blo[a] = std::min(blo[a], x[a]);
+          bhi[a] = std::max(bhi[a], x[a]);
+        }
+      }
+    }
+  }
+  const double pad = std::ldexp(r_all, -16);
+  for (int a = 0; a < 3; ++a) {
+    lo[a] = round_down(blo[a] - pad);
+    hi[a] = round_up(bhi[a] + pad);
+  }
+  return 0;
+}
+
+bool build_bvh(HostScene *S) {
+  S->bvh_nodes.clear();
+  S->bvh_pairs.clear();
+  S->bvh_depth = 0;
+  const double r_all = scene_coord_bound(*S);
+  Builder B;
+  for (int i = 0; i < S->nT; ++i) {
+    Prim p;
+    const int rc = acceptance_box(S->isect[(size_t)i], S->geom[(size_t)i], r_all, p.box.lo, p.box.hi);
+    if (rc < 0) {
+      S->bvh_status = "triangle " + std::to_string(i) + " has no bounded acceptance region";
+      return false;
+    }
+    if (rc == 1) continue;  // never accepted: left out of the tree
+    for (int a = 0; a < 3; ++a) p.c[a] = 0.5f * p.box.lo[a] + 0.5f * p.box.hi[a];
+    p.tri = i;
+    B.prims.push_back(p);
+  }
+  if (B.prims.size() < 2) {
+    S->bvh_status = "fewer than two hittable triangles";
+    return false;
+  }
+  Box root_box;
+  B.build(0, (int)B.prims.size(), 0, true, &root_box);
+  if (B.too_deep || B.nodes.size() >= 65535) {
+    S->bvh_status = "tree too deep or too large for the u16 traversal stack";
+    return false;
+  }
+  // leaves -> pairs (depth-first leaf order)
+  std::vector<int> leaf_code(B.leaves.size());
+  for (size_t l = 0; l < B.leaves.size(); ++l) {
+    const int b = B.leaves[l].first, e = B.leaves[l].second;
+    const int first = (int)S->bvh_pairs.size();
+    const int np = (e - b + 1) / 2;
+    if (first >= (1 << (31 - kBvhLeafPairBits))) {
+      S->bvh_status = "too many triangles for the leaf encoding";
+      S->bvh_pairs.clear();
+      return false;
+    }
+    for (int j = 0; j < np; ++j) {
+      BvhPair P;
+      std::memset(&P, 0, sizeof P);
+      for (int h = 0; h < 2; ++h) {
+        const int k = b + 2 * j + h;
+        if (k < e) {
+          const int t = B.prims[(size_t)k].tri;
+          put_tri(&P, h, &S->isect[(size_t)t], t);
+        } else {
+          put_tri(&P, h, nullptr, 0x7fffffff);
+        }
+      }
+      S->bvh_pairs.push_back(P);
+    }
+    leaf_code[l] = ~((first << kBvhLeafPairBits) | (np - 1));
+  }
+  // inner nodes -> breadth-first order
+  std::vector<int> order, newid(B.nodes.size(), -1);
+  order.push_back(0);
+  newid[0] = 0;
+  for (size_t h = 0; h < order.size(); ++h) {
+    const TNode &t = B.nodes[(size_t)order[h]];
+    for (int c = 0; c < 2; ++c)
+      if (t.kid[c] >= 0) {
+        newid[(size_t)t.kid[c]] = (int)order.size();
+        order.push_back(t.kid[c]);
+      }
+  }
+  S->bvh_nodes.resize(order.size());
+  for (size_t h = 0; h < order.size(); ++h) {
+    const TNode &t = B.nodes[(size_t)order[h]];
+    BvhNode &N = S->bvh_nodes[h];
+    std::memset(&N, 0, sizeof N);
+    const Box &b0 = t.box[0], &b1 = t.box[1];
+    const float q[12] = {b0.lo[0], b0.hi[0], b0.lo[1], b0.hi[1], b0.lo[2], b0.hi[2],
+                         b1.lo[0], b1.hi[0], b1.lo[1], b1.hi[1], b1.lo[2], b1.hi[2]};
+    std::memcpy(&N.q[0][0], q, sizeof q);
+    int kid[2];
+    for (int c = 0; c < 2; ++c) kid[c] = t.kid[c] >= 0 ? newid[(size_t)t.kid[c]] : leaf_code[(size_t)(~t.kid[c])];
+    std::memcpy(&N.q[3][0], kid, sizeof kid);
+  }
+  S->bvh_depth = B.max_depth;
+  S->bvh_status = "ok";
+  return true;
+}
+
+}  // namespace ipt

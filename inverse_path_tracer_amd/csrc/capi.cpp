@@ -188,6 +188,46 @@ int ipt_scene_camera(void *scene, float *out16) {
   return 0;
 }
 
+int ipt_scene_bvh_info(void *scene, int32_t *info4) {
+  GpuScene *s = as_scene(scene);
+  if (!s || !info4) return -1;
+  const ipt::HostScene &h = ipt::gpu_host(s);
+  info4[0] = (int32_t)h.bvh_nodes.size();
+  info4[1] = (int32_t)h.bvh_pairs.size();
+  info4[2] = h.bvh_depth;
+  info4[3] = ipt::gpu_accel_in_use(s);
+  if (h.bvh_nodes.empty()) fail("no BVH: " + h.bvh_status);
+  return h.bvh_nodes.empty() ? 0 : 1;
+}
+int ipt_scene_export_bvh(void *scene, float *nodes, float *pairs) {
+  GpuScene *s = as_scene(scene);
+  if (!s) return -1;
+  const ipt::HostScene &h = ipt::gpu_host(s);
+  if (nodes && !h.bvh_nodes.empty()) std::memcpy(nodes, h.bvh_nodes.data(), h.bvh_nodes.size() * sizeof(ipt::BvhNode));
+  if (pairs && !h.bvh_pairs.empty()) std::memcpy(pairs, h.bvh_pairs.data(), h.bvh_pairs.size() * sizeof(ipt::BvhPair));
+  return 0;
+}
+int ipt_scene_set_accel(void *scene, int mode) {
+  GpuScene *s = as_scene(scene);
+  if (!s) return -1;
+  return gpu_status(ipt::gpu_set_accel(s, mode));
+}
+int ipt_closest_hit_host(void *scene, int64_t n, const float *origins, const float *dirs, const int32_t *targets,
+                         float *t, int32_t *idx) {
+  GpuScene *s = as_scene(scene);
+  if (!s || n < 0 || (n > 0 && (!origins || !dirs || !t || !idx))) {
+    if (s) fail("ipt_closest_hit_host: bad arguments");
+    return -1;
+  }
+  return gpu_status(ipt::gpu_closest_hit_host(s, n, origins, dirs, targets, t, idx));
+}
+int ipt_closest_hit_dev(void *scene, int64_t n, const float *origins_dev, const float *dirs_dev,
+                        const int32_t *targets_dev, float *t_dev, int32_t *idx_dev, void *stream) {
+  GpuScene *s = as_scene(scene);
+  if (!s || n < 0) return -1;
+  return gpu_status(ipt::gpu_closest_hit(s, n, origins_dev, dirs_dev, targets_dev, t_dev, idx_dev, stream));
+}
+
 int ipt_scene_get_materials(void *scene, float *kd) {
   GpuScene *s = as_scene(scene);
   if (!s || !kd) return -1;

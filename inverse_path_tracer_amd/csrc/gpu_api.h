@@ -5,6 +5,7 @@
 
 #include <string>
 
+#include "../../include/ipt.h"  // IPT_ACCEL_* modes
 #include "scene_io.h"
 
 namespace ipt {
@@ -43,6 +44,16 @@ int gpu_render_samples_host(GpuScene *s, const RenderParams &p, float *samples);
 int gpu_render_host(GpuScene *s, const RenderParams &p, float *hdr, uint8_t *ldr);
 int gpu_adjoint_host(GpuScene *s, const RenderParams &p, const float *adj, double *grad);
 int gpu_graph_host(GpuScene *s, const RenderParams &p, const uint8_t *target, double *acc);
+
+// Acceleration structure (IPT_ACCEL_AUTO / _BRUTE / _BVH) and the one in use.
+int gpu_set_accel(GpuScene *s, int mode);
+int gpu_accel_in_use(const GpuScene *s);
+// Closest hit of n caller-supplied rays (origins, directions: n*3 floats;
+// targets: nullable, n ints, >= 0 = shadow ray towards that emitter).
+int gpu_closest_hit(GpuScene *s, int64_t n, const float *org_dev, const float *dir_dev, const int *targets_dev,
+                    float *t_dev, int *idx_dev, void *stream);
+int gpu_closest_hit_host(GpuScene *s, int64_t n, const float *org, const float *dir, const int *targets, float *t,
+                         int *idx);
 
 int gpu_device_count();
 int gpu_selftest_math(uint64_t n, uint64_t seed, uint64_t *counts);  // 8 mismatch counters

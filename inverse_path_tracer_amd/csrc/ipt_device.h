@@ -475,6 +475,140 @@ __device__ __forceinline__ int closest_hit_pairs(const TriPair *__restrict__ pai
   return bi;
 }
 
+// ------------------------------------------------------------ BVH closest hit
+// Exact replacement of the brute-force loop for large scenes (bvh.cpp states
+// why): per-lane stack traversal of the binary BVH, one ray per lane.  Node
+// boxes come from the workgroup's LDS copy (or global memory when the tree is
+// too big to stage), leaf triangle pairs through per-lane vector loads; the
+// leaf test is pair_ray's arithmetic, with the accept step keeping the
+// lexicographic minimum of (t, original triangle index) -- the result of the
+// reference's in-order strict-'<' loop, whatever order the leaves come in.
+struct BvhView {
+  const BvhNode *nodes;     // global copy
+  const float4 *lnodes;     // LDS copy (nullptr: read `nodes`)
+  const BvhPair *pairs;
+  const TriIsect *isect;    // original-order records (shadow target test)
+  uint32_t *stack;          // LDS, entry k of this lane at stack[k * kStride]
+};
+constexpr int kStackStride = 256;  // = the megakernel's block size
+constexpr int kBvhDone = (int)0x80000000;
+
+__device__ __forceinline__ void bvh_load_node(const BvhView &B, int n, float4 &q0, float4 &q1, float4 &q2,
+                                              float4 &q3) {
+  if (B.lnodes) {
+    const float4 *s = B.lnodes + 4 * n;
+    q0 = s[0];
+    q1 = s[1];
+    q2 = s[2];
+    q3 = s[3];
+  } else {
+    const float4 *s = reinterpret_cast<const float4 *>(B.nodes + n);
+    q0 = s[0];
+    q1 = s[1];
+    q2 = s[2];
+    q3 = s[3];
+  }
+}
+
+// One leaf pair with per-lane operands; accept = valid && (t, i) < (bt, bi).
+__device__ __forceinline__ void bvh_pair_test(const BvhPair &T, V3 p, V3 d, float &bt, int &bi) {
+  const f2 c0 = f2{T.f[0][0], T.f[0][1]}, c1 = f2{T.f[1][0], T.f[1][1]}, c2 = f2{T.f[2][0], T.f[2][1]};
+  const f2 n0 = f2{T.f[3][0], T.f[3][1]}, n1 = f2{T.f[4][0], T.f[4][1]}, n2 = f2{T.f[5][0], T.f[5][1]};
+  const f2 px = bc2(p.x) - c0, py = bc2(p.y) - c1, pz = bc2(p.z) - c2;
+  const f2 num = fma2(pz, n2, fma2(py, n1, px * n0));
+  const f2 denom = fma2(n2, bc2(d.z), fma2(n1, bc2(d.y), n0 * bc2(d.x)));
+  const f2 nb = denom;
+  const f2 r0 = f2{__builtin_amdgcn_rcpf(-denom.x), __builtin_amdgcn_rcpf(-denom.y)};
+  const f2 e0 = fma2(nb, r0, bc2(1.0f));
+  const f2 r1 = fma2(e0, r0, r0);
+  const f2 q0 = num * r1;
+  const f2 e1 = fma2(nb, q0, num);
+  const f2 q1 = fma2(e1, r1, q0);
+  const f2 e2 = fma2(nb, q1, num);
+  const f2 t = fma2(e2, r1, q1);
+  const f2 qx = fma2(bc2(d.x), t, bc2(p.x)), qy = fma2(bc2(d.y), t, bc2(p.y)), qz = fma2(bc2(d.z), t, bc2(p.z));
+  const f2 s0 = fma2(qz, f2{T.f[8][0], T.f[8][1]}, fma2(qy, f2{T.f[7][0], T.f[7][1]},
+                                                        fma2(qx, f2{T.f[6][0], T.f[6][1]}, f2{T.f[9][0], T.f[9][1]})));
+  const f2 s1 = fma2(qz, f2{T.f[12][0], T.f[12][1]}, fma2(qy, f2{T.f[11][0], T.f[11][1]},
+                                                          fma2(qx, f2{T.f[10][0], T.f[10][1]}, f2{T.f[13][0], T.f[13][1]})));
+  const f2 s2 = fma2(qz, f2{T.f[16][0], T.f[16][1]}, fma2(qy, f2{T.f[15][0], T.f[15][1]},
+                                                          fma2(qx, f2{T.f[14][0], T.f[14][1]}, f2{T.f[17][0], T.f[17][1]})));
+  const bool va = !(fabsf(denom.x) < kMinDotUp) && !(t.x < kEpsUp) && !(s0.x > 0.f) && !(s1.x > 0.f) && !(s2.x > 0.f);
+  const bool ta = va && (t.x < bt || (t.x == bt && T.idx[0] < bi));
+  bt = ta ? t.x : bt;
+  bi = ta ? T.idx[0] : bi;
+  const bool vb = !(fabsf(denom.y) < kMinDotUp) && !(t.y < kEpsUp) && !(s0.y > 0.f) && !(s1.y > 0.f) && !(s2.y > 0.f);
+  const bool tb = vb && (t.y < bt || (t.y == bt && T.idx[1] < bi));
+  bt = tb ? t.y : bt;
+  bi = tb ? T.idx[1] : bi;
+}
+
+// Closest hit through the BVH.  target < 0: ordinary cast.  target >= 0
+// (next-event shadow ray towards emitter triangle `target`): the caller only
+// needs to know whether the closest hit IS `target` (and its t), so the
+// target is tested first, its (t, index) seeds the search -- pruning every box
+// beyond it -- and the first triangle found ahead of it ends the traversal
+// (result != target, exactly as the full search would conclude).  Returns the
+// hit's original triangle index or -1.
+template <bool SHADOW>
+__device__ __forceinline__ int closest_hit_bvh(const BvhView &B, V3 p, V3 d, float &best_t, int target = -1) {
+  float bt = __builtin_inff();
+  int bi = -1;
+  if (SHADOW) {
+    hit_test(B.isect[target], target, p, d, bt, bi);
+    if (bi < 0) {
+      best_t = bt;
+      return -1;  // the target itself is missed: not the closest hit either
+    }
+  }
+  // slab parameters t = fma(box, 1/d, -p/d); |d| < 2^-60: slab ignored (NaN)
+  const float qnan = __builtin_nanf("");
+  const float ix = fabsf(d.x) < 0x1p-60f ? 0.f : __builtin_amdgcn_rcpf(d.x);
+  const float iy = fabsf(d.y) < 0x1p-60f ? 0.f : __builtin_amdgcn_rcpf(d.y);
+  const float iz = fabsf(d.z) < 0x1p-60f ? 0.f : __builtin_amdgcn_rcpf(d.z);
+  const float ox = fabsf(d.x) < 0x1p-60f ? qnan : -(p.x * ix);
+  const float oy = fabsf(d.y) < 0x1p-60f ? qnan : -(p.y * iy);
+  const float oz = fabsf(d.z) < 0x1p-60f ? qnan : -(p.z * iz);
+  const f2 ix2 = bc2(ix), iy2 = bc2(iy), iz2 = bc2(iz), ox2 = bc2(ox), oy2 = bc2(oy), oz2 = bc2(oz);
+  uint32_t *stk = B.stack;
+  int sp = 0;
+  int node = 0;
+  while (node != kBvhDone) {
+    while (node >= 0) {  // inner node: test both children's boxes
+      float4 q0, q1, q2, q3;
+      bvh_load_node(B, node, q0, q1, q2, q3);
+      const f2 tx0 = fma2(f2{q0.x, q1.z}, ix2, ox2), tx1 = fma2(f2{q0.y, q1.w}, ix2, ox2);
+      const f2 ty0 = fma2(f2{q0.z, q2.x}, iy2, oy2), ty1 = fma2(f2{q0.w, q2.y}, iy2, oy2);
+      const f2 tz0 = fma2(f2{q1.x, q2.z}, iz2, oz2), tz1 = fma2(f2{q1.y, q2.w}, iz2, oz2);
+      const float en0 = fmaxf(fmaxf(fminf(tx0.x, tx1.x), fminf(ty0.x, ty1.x)), fmaxf(fminf(tz0.x, tz1.x), 0.f));
+      const float ex0 = fminf(fminf(fmaxf(tx0.x, tx1.x), fmaxf(ty0.x, ty1.x)), fminf(fmaxf(tz0.x, tz1.x), bt));
+      const float en1 = fmaxf(fmaxf(fminf(tx0.y, tx1.y), fminf(ty0.y, ty1.y)), fmaxf(fminf(tz0.y, tz1.y), 0.f));
+      const float ex1 = fminf(fminf(fmaxf(tx0.y, tx1.y), fmaxf(ty0.y, ty1.y)), fminf(fmaxf(tz0.y, tz1.y), bt));
+      const bool h0 = en0 <= ex0, h1 = en1 <= ex1;
+      const int c0 = __float_as_int(q3.x), c1 = __float_as_int(q3.y);
+      if (h0 && h1) {
+        const bool first0 = en0 <= en1;
+        stk[sp * kStackStride] = (uint32_t)(first0 ? c1 : c0);
+        ++sp;
+        node = first0 ? c0 : c1;
+      } else if (h0 || h1) {
+        node = h0 ? c0 : c1;
+      } else {
+        node = sp > 0 ? (int)stk[--sp * kStackStride] : kBvhDone;
+      }
+    }
+    if (node != kBvhDone) {  // leaf
+      const int code = ~node;
+      const int first = code >> kBvhLeafPairBits, np = (code & ((1 << kBvhLeafPairBits) - 1)) + 1;
+      for (int j = 0; j < np; ++j) bvh_pair_test(B.pairs[first + j], p, d, bt, bi);
+      node = sp > 0 ? (int)stk[--sp * kStackStride] : kBvhDone;
+      if (SHADOW && bi != target) node = kBvhDone;  // occluded: decided
+    }
+  }
+  best_t = bt;
+  return bi;
+}
+
 // Triangle::getNormal (scene_basics.h:100-109)
 __device__ __forceinline__ V3 shading_normal(const TriGeom &g, V3 q) {
 #ifdef IPT_ABL_NORMAL  // timing-only ablation build

@@ -74,6 +74,14 @@ constexpr int kMaxAdjTris = 65535;  // tri and et share one 32-bit field
 constexpr int kEdgeW = 8;      // graph bin: w, w*f, pix[3]*w*f, light[3]*w*f
 constexpr int kMaxAdjBounces = 62;
 constexpr int kMaxTableTris = 512;  // kd/kd-over-pi LDS tables up to 12 KB
+constexpr int kLdsGradBytes = 16 * 1024;  // ADJ gradient bins in LDS up to nT = 682
+// Scenes of at least this many triangles trace through the BVH (auto mode).
+// Below it the unrolled / packed brute-force loop wins (a few pairs per cast).
+#ifndef IPT_BVH_MIN_TRIS
+#define IPT_BVH_MIN_TRIS 64
+#endif
+constexpr int kBvhMinTris = IPT_BVH_MIN_TRIS;
+constexpr int kBvhLdsNodeBytes = 32 * 1024;  // stage the whole tree in LDS up to 512 nodes
 
 struct TraceArgs {
   int W, H, spp, max_bounces;
@@ -91,6 +99,10 @@ struct TraceArgs {
   // instruction 64-bit division sequence
   int idx32;
   uint64_t m_spp, m_W, m_npix;
+  // BVH (BVH instances only): nodes staged in LDS (0: read from global),
+  // traversal stack entries per lane
+  int bvh_lds_nodes, bvh_stack;
+  int lds_grad;  // ADJ: gradient bins in LDS (else global fp64 atomics)
   float cam[16];
 };
 
@@ -118,11 +130,18 @@ using namespace dev;
 #ifndef IPT_MIN_BLOCKS_GRAPH
 #define IPT_MIN_BLOCKS_GRAPH 0
 #endif
-template <int MODE>
+// The BVH instances hold the traversal state on top (slab parameters, stack
+// pointer, node) and their LDS (node copy + stack) caps residency anyway:
+// 4 waves/SIMD, 128 VGPRs, no spill.
+#ifndef IPT_MIN_BLOCKS_BVH
+#define IPT_MIN_BLOCKS_BVH 4
+#endif
+template <int MODE, bool BVH>
 constexpr int min_blocks() {
-  return MODE == 0 ? IPT_MIN_BLOCKS_FWD : (MODE == 1 ? IPT_MIN_BLOCKS_ADJ : IPT_MIN_BLOCKS_GRAPH);
+  return BVH ? IPT_MIN_BLOCKS_BVH
+             : (MODE == 0 ? IPT_MIN_BLOCKS_FWD : (MODE == 1 ? IPT_MIN_BLOCKS_ADJ : IPT_MIN_BLOCKS_GRAPH));
 }
-#define IPT_TRACE_BOUNDS __attribute__((amdgpu_flat_work_group_size(1, kBlock), amdgpu_waves_per_eu(min_blocks<MODE>() ? min_blocks<MODE>() : 1)))
+#define IPT_TRACE_BOUNDS __attribute__((amdgpu_flat_work_group_size(1, kBlock), amdgpu_waves_per_eu(min_blocks<MODE, BVH>() ? min_blocks<MODE, BVH>() : 1)))
 // Profiling-only build (make variant DEFS=-DIPT_PHASE_TIMING): each wave
 // accumulates s_memtime cycles per phase of the loop; read with
 // ipt_debug_phase_cycles (tools/phase_timing.py).
@@ -141,7 +160,7 @@ __device__ unsigned long long g_phase_cycles[8];
 #ifndef IPT_SMALL_UNROLL
 #define IPT_SMALL_UNROLL 1
 #endif
-__device__ __forceinline__ int cast(const TriIsect *__restrict__ isect, const TriPair *__restrict__ pairs,
+__device__ __forceinline__ int cast_bf(const TriIsect *__restrict__ isect, const TriPair *__restrict__ pairs,
                                     const f2 *e3, int nT, V3 p, V3 d, float &t) {
 #if IPT_PAIRS
 #if IPT_SMALL_UNROLL
@@ -153,10 +172,26 @@ __device__ __forceinline__ int cast(const TriIsect *__restrict__ isect, const Tr
 #endif
 }
 
-template <int MODE, bool SPEC>
+// Closest hit of a path ray (target < 0) or of a shadow ray towards emitter
+// triangle `target` (only `result == target` and then t are used): the
+// brute-force loop for small scenes, the BVH for large ones.
+template <bool BVH>
+__device__ __forceinline__ int cast(const TriIsect *__restrict__ isect, const TriPair *__restrict__ pairs,
+                                    const f2 *e3, int nT, const BvhView &bv, V3 p, V3 d, float &t, int target) {
+  if (BVH) {
+    if (target >= 0) return closest_hit_bvh<true>(bv, p, d, t, target);
+    return closest_hit_bvh<false>(bv, p, d, t);
+  }
+  return cast_bf(isect, pairs, e3, nT, p, d, t);
+}
+
+// LDS carve-out of the BVH instances: node copy (16-B aligned) + stack.
+__host__ __device__ inline size_t bvh_lds_offset(size_t base) { return (base + 15) & ~(size_t)15; }
+
+template <int MODE, bool SPEC, bool BVH>
 __global__ IPT_TRACE_BOUNDS void trace_kernel(
     const TriIsect *__restrict__ isect, const TriPair *__restrict__ pairs, const TriGeom *__restrict__ geom,
-    const TriMat *__restrict__ mat,
+    const TriMat *__restrict__ mat, const BvhNode *__restrict__ bnodes, const BvhPair *__restrict__ bpairs,
     const float *__restrict__ kd, const int *__restrict__ emit_tri, const float *__restrict__ emit_cdf,
     const float *__restrict__ emit_pmf, const TraceArgs a, float *__restrict__ out_samples,
     const float *__restrict__ adj, double *__restrict__ grad, const uint8_t *__restrict__ target,
@@ -169,7 +204,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   double *lds_acc = lds;               // ADJ: nT*3 grad; GRAPH: (nT+1)*nT*kEdgeW bins
   int n_acc = 0;
   if (MODE == MODE_ADJ) {
-    n_acc = nT * 3;
+    n_acc = a.lds_grad ? nT * 3 : 0;
   } else if (MODE == MODE_GRAPH && a.lds_edges) {
     n_acc = (nT + 1) * nT * kEdgeW;
   }
@@ -201,9 +236,28 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     e3 = reinterpret_cast<const f2 *>(lds_e3);
   }
   float *lds_rec = lds_e3 + (a.small_pairs ? 6 * nP : 0);
+  BvhView bv;
+  bv.nodes = bnodes;
+  bv.pairs = bpairs;
+  bv.isect = isect;
+  bv.lnodes = nullptr;
+  bv.stack = nullptr;
+  if (BVH) {
+    const size_t rec_words = (MODE == MODE_ADJ) ? (size_t)vmax * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock : 0;
+    char *base = reinterpret_cast<char *>(lds);
+    const size_t off = bvh_lds_offset((size_t)(reinterpret_cast<char *>(lds_rec + rec_words) - base));
+    float4 *ln = reinterpret_cast<float4 *>(base + off);
+    if (a.bvh_lds_nodes > 0) {
+      const float4 *g = reinterpret_cast<const float4 *>(bnodes);
+      for (int i = tid; i < 4 * a.bvh_lds_nodes; i += kBlock) ln[i] = g[i];
+      bv.lnodes = ln;
+    }
+    bv.stack = reinterpret_cast<uint32_t *>(ln + 4 * a.bvh_lds_nodes) + tid;
+  }
   for (int i = tid; i < n_acc; i += kBlock) lds_acc[i] = 0.0;
   __syncthreads();
   double *acc = (MODE == MODE_GRAPH && !a.lds_edges) ? edges : lds_acc;
+  double *gacc = (MODE == MODE_ADJ && !a.lds_grad) ? grad : lds_acc;  // ADJ gradient bins
 
   // wave-uniform sample range (static partition, regenerated per lane)
   const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * kBlock + tid) >> 6);
@@ -303,7 +357,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     // ================= phase 1: path ray (radiance, path_trace.cu:111-144)
     float t = 0.f;
     int hit = -1;
-    if (active) hit = cast(isect, pairs, e3, nT, p, d, t);
+    if (active) hit = cast<BVH>(isect, pairs, e3, nT, bv, p, d, t, -1);
     PHASE(1)
     const bool vertex = active && hit >= 0;
     bool finished = false, escaped = false;
@@ -408,9 +462,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     if (__ballot(shadow)) {
       float ts = 0.f;
       int hs = -1;
-      if (shadow) hs = cast(isect, pairs, e3, nT, p, sd, ts);
-      PHASE(3)
       const int et = shadow ? emit_tri[emitter] : -1;
+      if (shadow) hs = cast<BVH>(isect, pairs, e3, nT, bv, p, sd, ts, et);
+      PHASE(3)
       if (shadow && hs == et) {  // must hit the sampled emitter itself
         const V3 ne = shading_normal(geom[et], along(p, sd, ts));
         const float ctp = -dot3(ne, sd);
@@ -576,9 +630,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
               const float cpi = ck / kPiF;
               gk = mk(gk.x + (cpi * Mk.x) * S.x, gk.y + (cpi * Mk.y) * S.y, gk.z + (cpi * Mk.z) * S.z);
             }
-            atomicAdd(&lds_acc[tk * 3 + 0], (double)(ax * gk.x));
-            atomicAdd(&lds_acc[tk * 3 + 1], (double)(ay * gk.y));
-            atomicAdd(&lds_acc[tk * 3 + 2], (double)(az * gk.z));
+            atomicAdd(&gacc[tk * 3 + 0], (double)(ax * gk.x));
+            atomicAdd(&gacc[tk * 3 + 1], (double)(ay * gk.y));
+            atomicAdd(&gacc[tk * 3 + 2], (double)(az * gk.z));
             float dx, dy, dz, tx, ty, tz;
             ddir(tk, sdk, dx, dy, dz);
             tdiff(tk, si, tx, ty, tz);
@@ -597,7 +651,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
 
   if (MODE != MODE_FWD) {
     __syncthreads();
-    if (!(MODE == MODE_GRAPH && !a.lds_edges)) {
+    if (n_acc > 0) {
       double *dstp = (MODE == MODE_ADJ) ? grad : edges;
       for (int i = tid; i < n_acc; i += kBlock) {
         const double v = lds_acc[i];
@@ -672,8 +726,11 @@ struct GpuScene {
   float *ws = nullptr;  // per-sample radiance workspace
   size_t ws_bytes = 0;
   bool has_ks = false;      // some material has a Phong lobe
-  int grid[6] = {0, 0, 0, 0, 0, 0};  // resident workgroups per (mode, spec) (0 = not queried)
-  size_t grid_lds[6] = {0, 0, 0, 0, 0, 0};
+  BvhNode *bnodes = nullptr;
+  BvhPair *bpairs = nullptr;
+  int accel = IPT_ACCEL_AUTO;
+  int grid[12] = {0};       // resident workgroups per (mode, spec, bvh) (0 = not queried)
+  size_t grid_lds[12] = {0};
 };
 
 #ifdef IPT_PHASE_TIMING
@@ -707,7 +764,7 @@ GpuScene *gpu_upload(const HostScene &host, std::string *err) {
   pack_pairs(host.isect.data(), (int)host.isect.size(), pairs.data());
   if (upload(&s->isect, host.isect) || upload(&s->pairs, pairs) || upload(&s->geom, host.geom) || upload(&s->mat, host.mat) ||
       upload(&s->kd, host.kd) || upload(&s->emit_tri, host.emit_tri) || upload(&s->emit_cdf, host.emit_cdf) ||
-      upload(&s->emit_pmf, host.emit_pmf)) {
+      upload(&s->emit_pmf, host.emit_pmf) || upload(&s->bnodes, host.bvh_nodes) || upload(&s->bpairs, host.bvh_pairs)) {
     *err = gpu_last_error();
     gpu_free(s);
     return nullptr;
@@ -739,6 +796,8 @@ void gpu_free(GpuScene *s) {
   (void)hipFree(s->emit_cdf);
   (void)hipFree(s->emit_pmf);
   (void)hipFree(s->ws);
+  (void)hipFree(s->bnodes);
+  (void)hipFree(s->bpairs);
   delete s;
 }
 
@@ -776,12 +835,12 @@ static int check_params(const GpuScene *s, const RenderParams &p) {
   return 0;
 }
 
-template <int MODE, bool SPEC>
+template <int MODE, bool SPEC, bool BVH>
 static int resident_grid(GpuScene *s, size_t lds_bytes, int *grid) {
-  const int slot = MODE * 2 + (SPEC ? 1 : 0);
+  const int slot = MODE * 4 + (SPEC ? 2 : 0) + (BVH ? 1 : 0);
   if (s->grid[slot] == 0 || s->grid_lds[slot] != lds_bytes) {
     int per_cu = 0, cus = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<MODE, SPEC>, kBlock, lds_bytes));
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<MODE, SPEC, BVH>, kBlock, lds_bytes));
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device));
     if (per_cu <= 0) {
       gpu_set_error("trace kernel cannot be resident (LDS request too large?)");
@@ -790,8 +849,8 @@ static int resident_grid(GpuScene *s, size_t lds_bytes, int *grid) {
     s->grid[slot] = per_cu * cus;
     s->grid_lds[slot] = lds_bytes;
     if (std::getenv("IPT_DEBUG_GRID"))
-      std::fprintf(stderr, "[ipt] trace_kernel<%d,%d>: %zu B LDS/block, %d blocks/CU x %d CUs\n", MODE, (int)SPEC,
-                   lds_bytes, per_cu, cus);
+      std::fprintf(stderr, "[ipt] trace_kernel<%d,%d,%d>: %zu B LDS/block, %d blocks/CU x %d CUs\n", MODE, (int)SPEC,
+                   (int)BVH, lds_bytes, per_cu, cus);
   }
   *grid = s->grid[slot];
   return 0;
@@ -819,8 +878,29 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.m_spp = p.spp > 1 ? ~0ull / (uint64_t)p.spp + 1 : 0;
   a.m_W = p.width > 1 ? ~0ull / (uint64_t)p.width + 1 : 0;
   a.m_npix = a.npix > 1 ? ~0ull / a.npix + 1 : 0;
+  a.bvh_lds_nodes = 0;
+  a.bvh_stack = 0;
+  a.lds_grad = 1;
   std::memcpy(a.cam, s->host.cam, sizeof a.cam);
   return a;
+}
+
+// Acceleration structure of a launch: the BVH when the scene has one and is
+// past the brute-force size (or the caller forced it), else the pair loop.
+static bool use_bvh(const GpuScene *s) {
+  if (s->host.bvh_nodes.empty()) return false;
+  if (s->accel == IPT_ACCEL_BVH) return true;
+  if (s->accel == IPT_ACCEL_BRUTE) return false;
+  return s->host.nT >= kBvhMinTris;
+}
+
+// BVH LDS carve-out on top of `base` bytes; fills the args' BVH fields.
+static size_t bvh_lds(const GpuScene *s, TraceArgs &a, size_t base) {
+  const size_t nn = s->host.bvh_nodes.size();
+  a.bvh_lds_nodes = nn * sizeof(BvhNode) <= (size_t)kBvhLdsNodeBytes ? (int)nn : 0;
+  a.bvh_stack = std::max(1, s->host.bvh_depth);
+  return bvh_lds_offset(base) + (size_t)a.bvh_lds_nodes * sizeof(BvhNode) +
+         (size_t)a.bvh_stack * kBlock * sizeof(uint32_t);
 }
 
 static size_t table_bytes(const TraceArgs &a) {
@@ -828,27 +908,37 @@ static size_t table_bytes(const TraceArgs &a) {
          (a.small_pairs ? (size_t)6 * ((a.nT + 1) / 2) * sizeof(float) : 0);
 }
 
-template <int MODE, bool SPEC>
+template <int MODE, bool SPEC, bool BVH>
 static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float *kd_dev, float *out, const float *adj,
                        double *grad, const uint8_t *target, double *edges, hipStream_t st) {
   int grid = 0;
-  if (resident_grid<MODE, SPEC>(s, lds, &grid)) return -1;
+  if (lds > 160 * 1024) {
+    gpu_set_error("LDS footprint of the launch exceeds 160 KiB");
+    return -1;
+  }
+  if (resident_grid<MODE, SPEC, BVH>(s, lds, &grid)) return -1;
   if (a.n_samples == 0) return 0;
-  hipLaunchKernelGGL((trace_kernel<MODE, SPEC>), dim3(grid), dim3(kBlock), lds, st, s->isect, s->pairs, s->geom, s->mat,
-                     kd_dev ? kd_dev : s->kd, s->emit_tri, s->emit_cdf, s->emit_pmf, a, out, adj, grad, target,
-                     edges);
+  hipLaunchKernelGGL((trace_kernel<MODE, SPEC, BVH>), dim3(grid), dim3(kBlock), lds, st, s->isect, s->pairs, s->geom,
+                     s->mat, s->bnodes, s->bpairs, kd_dev ? kd_dev : s->kd, s->emit_tri, s->emit_cdf, s->emit_pmf, a,
+                     out, adj, grad, target, edges);
   HIP_TRY(hipGetLastError());
   return 0;
 }
 
 // The Phong paths (double-precision pow) are compiled only into the SPEC
 // instance, used when some material has Ks != 0; the shipped scenes have
-// none, and dropping the code lowers register pressure (occupancy).
+// none, and dropping the code lowers register pressure (occupancy).  The BVH
+// instances carry the traversal (and its LDS) only for large scenes.
 template <int MODE>
-static int launch(GpuScene *s, const TraceArgs &a, size_t lds, const float *kd_dev, float *out, const float *adj,
+static int launch(GpuScene *s, TraceArgs a, size_t lds, const float *kd_dev, float *out, const float *adj,
                   double *grad, const uint8_t *target, double *edges, hipStream_t st) {
-  if (s->has_ks) return launch_inst<MODE, true>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
-  return launch_inst<MODE, false>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
+  if (use_bvh(s)) {
+    lds = bvh_lds(s, a, lds);
+    if (s->has_ks) return launch_inst<MODE, true, true>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
+    return launch_inst<MODE, false, true>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
+  }
+  if (s->has_ks) return launch_inst<MODE, true, false>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
+  return launch_inst<MODE, false, false>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
 }
 
 int gpu_render_samples(GpuScene *s, const RenderParams &p, const float *kd_dev, float *samples_dev, void *stream) {
@@ -917,8 +1007,9 @@ int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const f
     gpu_set_error("adjoint supports at most 65535 triangles");
     return -1;
   }
-  const TraceArgs a = make_args(s, p);
-  const size_t lds = (size_t)s->host.nT * 3 * sizeof(double) + table_bytes(a) +
+  TraceArgs a = make_args(s, p);
+  a.lds_grad = (size_t)s->host.nT * 3 * sizeof(double) <= (size_t)kLdsGradBytes ? 1 : 0;
+  const size_t lds = (a.lds_grad ? (size_t)s->host.nT * 3 * sizeof(double) : 0) + table_bytes(a) +
                      (size_t)(p.max_bounces + 1) * (s->has_ks ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock *
                          sizeof(float);
   if (lds > 160 * 1024) {
@@ -1046,6 +1137,103 @@ int gpu_selftest_math(uint64_t n, uint64_t seed, uint64_t *counts_host) {
   return rc;
 }
 
+// ------------------------------------------------------------ closest-hit probe
+// The cast() of the megakernel on caller-supplied rays: one ray per thread,
+// the same LDS staging (small-scene plane offsets, BVH nodes + stack).
+// targets[i] >= 0 makes ray i a shadow ray towards that emitter triangle
+// (the BVH then answers only "is the closest hit the target, and at which
+// t"; the brute-force loop always returns the full closest hit).  Used by
+// the exactness tests of the BVH against the brute-force loop.
+template <bool BVH>
+__global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__restrict__ isect,
+                                                             const TriPair *__restrict__ pairs,
+                                                             const BvhNode *__restrict__ bnodes,
+                                                             const BvhPair *__restrict__ bpairs, int nT, int small,
+                                                             int lds_nodes, int64_t n, const float *__restrict__ org,
+                                                             const float *__restrict__ dir,
+                                                             const int *__restrict__ targets, float *__restrict__ t_out,
+                                                             int *__restrict__ i_out) {
+  extern __shared__ double lds[];
+  const int tid = threadIdx.x;
+  const int nP = (nT + 1) >> 1;
+  float *lds_e3 = reinterpret_cast<float *>(lds);
+  const f2 *e3 = nullptr;
+  if (small) {
+    for (int i = tid; i < 6 * nP; i += kBlock) {
+      const int j = i / 6, kf = (i % 6) >> 1, h = i & 1;
+      lds_e3[i] = pairs[j].f[9 + 4 * kf][h];
+    }
+    e3 = reinterpret_cast<const f2 *>(lds_e3);
+  }
+  BvhView bv;
+  bv.nodes = bnodes;
+  bv.pairs = bpairs;
+  bv.isect = isect;
+  bv.lnodes = nullptr;
+  bv.stack = nullptr;
+  if (BVH) {
+    char *base = reinterpret_cast<char *>(lds);
+    float4 *ln = reinterpret_cast<float4 *>(base + bvh_lds_offset((size_t)(small ? 6 * nP : 0) * sizeof(float)));
+    if (lds_nodes > 0) {
+      const float4 *g = reinterpret_cast<const float4 *>(bnodes);
+      for (int i = tid; i < 4 * lds_nodes; i += kBlock) ln[i] = g[i];
+      bv.lnodes = ln;
+    }
+    bv.stack = reinterpret_cast<uint32_t *>(ln + 4 * lds_nodes) + tid;
+  }
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * kBlock + tid;
+  if (i >= n) return;
+  const V3 p = mk(org[3 * i], org[3 * i + 1], org[3 * i + 2]);
+  const V3 d = mk(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);
+  const int target = targets ? targets[i] : -1;
+  float t = 0.f;
+  const int h = cast<BVH>(isect, pairs, e3, nT, bv, p, d, t, target);
+  t_out[i] = t;
+  i_out[i] = h;
+}
+
+int gpu_set_accel(GpuScene *s, int mode) {
+  if (mode != IPT_ACCEL_AUTO && mode != IPT_ACCEL_BRUTE && mode != IPT_ACCEL_BVH) {
+    gpu_set_error("unknown acceleration mode");
+    return -1;
+  }
+  if (mode == IPT_ACCEL_BVH && s->host.bvh_nodes.empty()) {
+    gpu_set_error("scene has no BVH: " + s->host.bvh_status);
+    return -1;
+  }
+  s->accel = mode;
+  return 0;
+}
+int gpu_accel_in_use(const GpuScene *s) { return use_bvh(s) ? IPT_ACCEL_BVH : IPT_ACCEL_BRUTE; }
+
+int gpu_closest_hit(GpuScene *s, int64_t n, const float *org_dev, const float *dir_dev, const int *targets_dev,
+                    float *t_dev, int *idx_dev, void *stream) {
+  if (!s->on_device) {
+    gpu_set_error("scene was loaded host-only (ipt_load_scene_host); it cannot be traced");
+    return -1;
+  }
+  if (n <= 0) return 0;
+  TraceArgs a;
+  std::memset(&a, 0, sizeof a);
+  a.nT = s->host.nT;
+  const int small = (IPT_PAIRS && IPT_SMALL_UNROLL && s->host.nT <= 2 * kSmallPairs) ? 1 : 0;
+  const size_t base = small ? (size_t)6 * ((s->host.nT + 1) / 2) * sizeof(float) : 0;
+  const int blocks = (int)((n + kBlock - 1) / kBlock);
+  if (use_bvh(s)) {
+    const size_t lds = bvh_lds(s, a, base);
+    hipLaunchKernelGGL(closest_hit_kernel<true>, dim3(blocks), dim3(kBlock), lds, (hipStream_t)stream, s->isect,
+                       s->pairs, s->bnodes, s->bpairs, s->host.nT, small, a.bvh_lds_nodes, n, org_dev, dir_dev,
+                       targets_dev, t_dev, idx_dev);
+  } else {
+    hipLaunchKernelGGL(closest_hit_kernel<false>, dim3(blocks), dim3(kBlock), base, (hipStream_t)stream, s->isect,
+                       s->pairs, s->bnodes, s->bpairs, s->host.nT, small, 0, n, org_dev, dir_dev, targets_dev, t_dev,
+                       idx_dev);
+  }
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
 // ------------------------------------------------------------ host wrappers
 namespace {
 struct DevBuf {
@@ -1088,6 +1276,29 @@ int gpu_adjoint_host(GpuScene *s, const RenderParams &p, const float *adj, doubl
   HIP_TRY(hipMemset(g.p, 0, ng * sizeof(double)));
   if (gpu_adjoint(s, p, nullptr, (const float *)a.p, (double *)g.p, nullptr)) return -1;
   HIP_TRY(hipMemcpy(grad, g.p, ng * sizeof(double), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int gpu_closest_hit_host(GpuScene *s, int64_t n, const float *org, const float *dir, const int *targets, float *t,
+                         int *idx) {
+  if (n <= 0) return 0;
+  DevBuf o, d, g, tt, ii;
+  const size_t n3 = (size_t)n * 3 * sizeof(float);
+  HIP_TRY(hipMalloc(&o.p, n3));
+  HIP_TRY(hipMalloc(&d.p, n3));
+  HIP_TRY(hipMalloc(&tt.p, (size_t)n * sizeof(float)));
+  HIP_TRY(hipMalloc(&ii.p, (size_t)n * sizeof(int)));
+  HIP_TRY(hipMemcpy(o.p, org, n3, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(d.p, dir, n3, hipMemcpyHostToDevice));
+  if (targets) {
+    HIP_TRY(hipMalloc(&g.p, (size_t)n * sizeof(int)));
+    HIP_TRY(hipMemcpy(g.p, targets, (size_t)n * sizeof(int), hipMemcpyHostToDevice));
+  }
+  if (gpu_closest_hit(s, n, (const float *)o.p, (const float *)d.p, (const int *)g.p, (float *)tt.p, (int *)ii.p,
+                      nullptr))
+    return -1;
+  HIP_TRY(hipMemcpy(t, tt.p, (size_t)n * sizeof(float), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(idx, ii.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));
   return 0;
 }
 

@@ -25,6 +25,8 @@
 // -ffp-contract=off); DESIGN.md §3.
 #include "scene_io.h"
 
+#include "bvh.h"
+
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
@@ -732,6 +734,7 @@ bool build_scene(const std::vector<ObjectRecord> &objects, HostScene *out, std::
     S.emit_pmf.push_back(p);
   }
   camera_matrix(S.cam);
+  build_bvh(&S);  // no BVH (bvh_status says why) keeps the brute-force loop
   return true;
 }
 

@@ -27,6 +27,11 @@ struct HostScene {
   std::vector<float> emit_pmf;  // nE
   std::vector<int> obj_first, obj_count;
   float cam[16];
+  // triangle BVH (bvh.cpp); empty when the scene cannot use one exactly
+  std::vector<BvhNode> bvh_nodes;
+  std::vector<BvhPair> bvh_pairs;
+  int bvh_depth = 0;           // inner-node levels (stack entries needed)
+  std::string bvh_status;      // "ok" or why the BVH was not built
 };
 
 // Builds the scene (scene.h:89-117 Scene::Scene semantics).  Returns false

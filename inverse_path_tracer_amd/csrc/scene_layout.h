@@ -87,6 +87,38 @@ struct TriMat {         // 8 floats
 };
 static_assert(sizeof(TriMat) == 32, "TriMat layout");
 
+// ---- triangle BVH (bvh.cpp) for scenes past the brute-force size
+// The reference's BVH (bvh.h:109-205) is over OBJECTS and, for the shipped
+// scenes (<= 4 objects), a single leaf: its closest hit is brute force over
+// every triangle with first-index ties (scene_basics.h:444, bvh.h:75).  This
+// BVH is over triangles and returns exactly that hit: boxes bound the region
+// where the fp32 hit test can ACCEPT a point (not the triangle itself), and
+// the traversal keeps the lexicographic minimum of (t, triangle index).
+//
+// Binary node, Aila-Laine layout: both children's boxes live in the parent,
+// so one 64-B fetch (four 16-B LDS reads) tests two boxes.
+//   q[0] = lo0.x hi0.x lo0.y hi0.y   q[1] = lo0.z hi0.z lo1.x hi1.x
+//   q[2] = lo1.y hi1.y lo1.z hi1.z   q[3] = child0 child1 (int bits) 0 0
+// child >= 0: inner node index; child < 0: leaf, ~child = first_pair << 4 |
+// (pairs - 1).  Nodes are stored breadth-first (root 0), so a prefix of the
+// array is the top of the tree.
+struct BvhNode {
+  float q[4][4];
+};
+static_assert(sizeof(BvhNode) == 64, "BvhNode layout");
+constexpr int kBvhLeafPairBits = 4;   // <= 16 triangle pairs per leaf
+constexpr int kBvhMaxDepth = 32;      // traversal stack entries (u16, LDS)
+// Leaf triangles, two per record in TriPair's field order, plus the ORIGINAL
+// triangle indices (the tie-break key and the returned hit index).  An odd
+// leaf is padded with an all-zero triangle (never accepted) of index
+// 0x7fffffff.
+struct BvhPair {
+  float f[18][2];
+  int32_t idx[2];
+  int32_t pad[2];
+};
+static_assert(sizeof(BvhPair) == 160, "BvhPair layout");
+
 // Device view of a loaded scene (all pointers are device pointers).
 struct DevScene {
   int nT, nE;

@@ -144,6 +144,46 @@ class Scene:
         N.check(N.lib().ipt_scene_camera(self.handle, out.ctypes.data_as(N.fp)), "camera")
         return out.reshape(4, 4)
 
+    # ---------------------------------------------------------- acceleration
+    def set_accel(self, mode: int):
+        """IPT_ACCEL_AUTO / _BRUTE / _BVH (N.ACCEL_*): which closest-hit loop
+        the kernels run.  Results are identical; only speed differs."""
+        N.check(N.lib().ipt_scene_set_accel(self.handle, int(mode)), "set_accel")
+
+    def bvh_info(self) -> dict:
+        info = (C.c_int32 * 4)()
+        has = N.lib().ipt_scene_bvh_info(self.handle, info)
+        N.check(has, "bvh_info")
+        return {"has_bvh": bool(has), "nodes": info[0], "pairs": info[1], "depth": info[2],
+                "accel": {N.ACCEL_BRUTE: "brute", N.ACCEL_BVH: "bvh"}.get(info[3], "?"),
+                "status": "ok" if has else N.last_error()}
+
+    def export_bvh(self):
+        """(nodes[n,16] float32, pairs[m,40] float32) -- BvhNode / BvhPair
+        records (scene_layout.h); child links and indices are int32 bits."""
+        i = self.bvh_info()
+        nodes = np.zeros((i["nodes"], 16), np.float32)
+        pairs = np.zeros((i["pairs"], 40), np.float32)
+        N.check(N.lib().ipt_scene_export_bvh(self.handle, nodes.ctypes.data_as(N.fp), pairs.ctypes.data_as(N.fp)),
+                "export_bvh")
+        return nodes, pairs
+
+    def closest_hit(self, origins, dirs, targets=None):
+        """The kernels' cast on caller rays: (t float32[n], idx int32[n])."""
+        o = np.ascontiguousarray(np.asarray(origins, np.float32).reshape(-1, 3))
+        d = np.ascontiguousarray(np.asarray(dirs, np.float32).reshape(-1, 3))
+        n = o.shape[0]
+        t = np.zeros(n, np.float32)
+        idx = np.zeros(n, np.int32)
+        tg = None
+        if targets is not None:
+            tg = np.ascontiguousarray(np.asarray(targets, np.int32).reshape(n))
+        ip = C.POINTER(C.c_int32)
+        N.check(N.lib().ipt_closest_hit_host(self.handle, n, o.ctypes.data_as(N.fp), d.ctypes.data_as(N.fp),
+                                             tg.ctypes.data_as(ip) if tg is not None else None,
+                                             t.ctypes.data_as(N.fp), idx.ctypes.data_as(ip)), "closest_hit")
+        return t, idx
+
     # ---------------------------------------------------------- host-memory renders
     def render_samples(self, width, height, spp, max_bounces=None, seed=0, row_begin=0, row_end=None):
         p = N.make_params(width, height, spp, max_bounces, seed, row_begin, row_end)

@@ -1182,6 +1182,45 @@ static hit_t intersect(const oscene_t *sc, ray_t r) {
   }
   return best;
 }
+/* Closest hit of caller rays (the parity anchor of the kernels' BVH). */
+int oro_closest_hit(void *p, int64_t n, const float *org, const float *dir, float *t, int *idx) {
+  const oscene_t *sc = (const oscene_t *)p;
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; i++) {
+    ray_t r;
+    r.p = mk(org[3 * i], org[3 * i + 1], org[3 * i + 2]);
+    r.d = mk(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);
+    hit_t h = intersect(sc, r);
+    t[i] = h.t;
+    idx[i] = h.tri;
+  }
+  return 0;
+}
+/* The single-triangle test of intersect() without the best-t condition:
+ * t_out[i] = the t at which triangle i accepts the ray, NaN if it rejects.
+ * Test infrastructure for the BVH's acceptance-region bound. */
+int oro_hit_each(void *p, const float *org, const float *dir, float *t_out) {
+  const oscene_t *sc = (const oscene_t *)p;
+  ray_t r;
+  r.p = mk(org[0], org[1], org[2]);
+  r.d = mk(dir[0], dir[1], dir[2]);
+  for (int i = 0; i < sc->nT; i++) {
+    const otri_t *t = &sc->tris[i];
+    t_out[i] = NAN;
+    float denom = dot3(t->n, r.d);
+    if ((double)fabsf(denom) < MIN_DOT) continue;
+    float tt = dot3(sub(r.p, t->c), t->n) / -denom;
+    if ((double)tt < EPSILON_T) continue;
+    v3 q = mk(fmaf(r.d.x, tt, r.p.x), fmaf(r.d.y, tt, r.p.y), fmaf(r.d.z, tt, r.p.z));
+    int inside = 1;
+    for (int j = 0; j < 3; j++) {
+      float sd = fmaf(q.z, t->eo[j].z, fmaf(q.y, t->eo[j].y, fmaf(q.x, t->eo[j].x, t->ed[j])));
+      if (sd > 0.f) { inside = 0; break; }
+    }
+    if (inside) t_out[i] = tt;
+  }
+  return 0;
+}
 static v3 hit_point(ray_t r, float t) {
   return mk(fmaf(r.d.x, t, r.p.x), fmaf(r.d.y, t, r.p.y), fmaf(r.d.z, t, r.p.z));
 }

@@ -82,6 +82,14 @@ int oro_adjoint(void *scene, int W, int H, int spp, int max_bounces,
                 uint64_t seed, int row_begin, int row_end, const float *adj,
                 double *grad);
 
+/* Closest hit (BVH::getIntersection over its single leaf, bvh.h:55-77 ->
+ * Object::getIntersection, scene_basics.h:426-459) of n caller rays:
+ * t[i] (INFINITY on a miss), idx[i] (-1 on a miss). */
+int oro_closest_hit(void *scene, int64_t n, const float *org, const float *dir, float *t, int *idx);
+/* Per-triangle acceptance of one ray (no best-t test): t_out[nT], NaN where
+ * the triangle rejects the ray. */
+int oro_hit_each(void *scene, const float *org, const float *dir, float *t_out);
+
 /* Canonical scalar helpers, exported so the tests can pin them. */
 float oro_uniform_at(uint64_t seed, int k); /* k-th curand_uniform draw */
 void oro_sincos(float x, float *s, float *c);

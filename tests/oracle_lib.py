@@ -52,6 +52,9 @@ def lib():
         L.oro_powf.restype = C.c_float
         L.oro_powf.argtypes = [C.c_float, C.c_float]
         L.oro_set_threads.argtypes = [C.c_int]
+        ip = C.POINTER(C.c_int)
+        L.oro_closest_hit.argtypes = [vp, i64, fp, fp, fp, ip]
+        L.oro_hit_each.argtypes = [vp, fp, fp, fp]
         _lib = L
     return _lib
 
@@ -143,6 +146,23 @@ class OracleScene:
         if rc:
             raise RuntimeError(lib().oro_last_error().decode())
         return grad
+
+
+    def closest_hit(self, origins, dirs):
+        o = np.ascontiguousarray(np.asarray(origins, np.float32).reshape(-1, 3))
+        d = np.ascontiguousarray(np.asarray(dirs, np.float32).reshape(-1, 3))
+        n = o.shape[0]
+        t = np.zeros(n, np.float32)
+        idx = np.zeros(n, np.int32)
+        lib().oro_closest_hit(self.ptr, n, _fp(o), _fp(d), _fp(t), idx.ctypes.data_as(C.POINTER(C.c_int)))
+        return t, idx
+
+    def hit_each(self, origin, direction):
+        o = np.ascontiguousarray(np.asarray(origin, np.float32).reshape(3))
+        d = np.ascontiguousarray(np.asarray(direction, np.float32).reshape(3))
+        t = np.zeros(lib().oro_num_triangles(self.ptr), np.float32)
+        lib().oro_hit_each(self.ptr, _fp(o), _fp(d), _fp(t))
+        return t
 
 
 def pixel_mean(samples, npix, spp):

@@ -401,3 +401,112 @@ def test_large_scene_adjoint_and_graph(oracle):
     acc_q, data_q = Q.graph(W, H, 2, 3, 4, tgt)
     np.testing.assert_allclose(acc, acc_q, rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(data, data_q, rtol=1e-6, atol=1e-7)
+
+
+# ------------------------------------------------------------- triangle BVH
+def _bvh_scene(recs):
+    from test_bvh import CLUTTER_SCENE, SPHERE_SCENE  # noqa: F401
+
+    P = product_scene(recs)
+    assert P.bvh_info()["accel"] == "bvh"
+    return P
+
+
+def _rays(P, n_adv, n_rand, seed):
+    from test_bvh import _adversarial_rays
+
+    tris = P.triangles()
+    cam_origin = P.camera()[:3, 3].astype(np.float64)
+    rng = np.random.RandomState(seed)
+    O, D = _adversarial_rays(tris, cam_origin, rng, n_adv)
+    v = tris[:, 0:9].reshape(-1, 3)
+    lo, hi = v.min(0), v.max(0)
+    Or = rng.uniform(lo, hi, (n_rand, 3)).astype(np.float32)
+    Dr = rng.normal(size=(n_rand, 3))
+    Dr = (Dr / np.linalg.norm(Dr, axis=1, keepdims=True)).astype(np.float32)
+    return np.concatenate([O, Or]), np.concatenate([D, Dr])
+
+
+@pytest.mark.parametrize("which", ["sphere", "clutter"])
+def test_bvh_closest_hit_equals_brute_force(oracle, which):
+    """The device BVH cast returns the brute-force loop's hit bit-for-bit
+    (index and t) on adversarial + random rays, and both equal the oracle."""
+    from inverse_path_tracer_amd import _native as N
+    from test_bvh import CLUTTER_SCENE, SPHERE_SCENE
+
+    recs = SPHERE_SCENE if which == "sphere" else CLUTTER_SCENE
+    P = _bvh_scene(recs)
+    O, D = _rays(P, 20000, 400000, 3 if which == "sphere" else 4)
+    P.set_accel(N.ACCEL_BVH)
+    tb, ib = P.closest_hit(O, D)
+    P.set_accel(N.ACCEL_BRUTE)
+    tf, i_f = P.closest_hit(O, D)
+    P.set_accel(N.ACCEL_AUTO)
+    assert np.array_equal(ib, i_f)
+    assert np.array_equal(bits(tb), bits(tf))
+    assert (ib >= 0).mean() > 0.5
+    Q = oracle.OracleScene(recs)
+    tq, iq = Q.closest_hit(O[:60000], D[:60000])
+    assert np.array_equal(iq, ib[:60000])
+    hit = iq >= 0
+    assert np.array_equal(bits(tq[hit]), bits(tb[:60000][hit]))
+
+
+def test_bvh_shadow_query_equals_brute_force():
+    """Shadow rays (target = an emitter triangle): the BVH's early-out answer
+    "closest hit is the target, at t" equals the full brute-force search."""
+    from inverse_path_tracer_amd import _native as N
+    from test_bvh import SPHERE_SCENE
+
+    P = _bvh_scene(SPHERE_SCENE)
+    tris = P.triangles()
+    emit = np.nonzero(tris[:, 56] >= 0)[0]
+    assert len(emit) == 2
+    rng = np.random.RandomState(12)
+    n = 300000
+    v = tris[:, 0:9].reshape(-1, 3, 3)
+    src = rng.randint(0, P.nT, n)
+    a, b = rng.uniform(0, 1, (2, n))
+    flip = a + b > 1
+    a[flip], b[flip] = 1 - a[flip], 1 - b[flip]
+    O = v[src, 0] + a[:, None] * (v[src, 1] - v[src, 0]) + b[:, None] * (v[src, 2] - v[src, 0])
+    tg = emit[rng.randint(0, 2, n)]
+    a2, b2 = rng.uniform(0, 1, (2, n))
+    flip = a2 + b2 > 1
+    a2[flip], b2[flip] = 1 - a2[flip], 1 - b2[flip]
+    pt = v[tg, 0] + a2[:, None] * (v[tg, 1] - v[tg, 0]) + b2[:, None] * (v[tg, 2] - v[tg, 0])
+    D = pt - O
+    D /= np.linalg.norm(D, axis=1, keepdims=True)
+    O, D = O.astype(np.float32), D.astype(np.float32)
+    P.set_accel(N.ACCEL_BVH)
+    tb, ib = P.closest_hit(O, D, targets=tg)
+    P.set_accel(N.ACCEL_BRUTE)
+    tf, i_f = P.closest_hit(O, D)
+    P.set_accel(N.ACCEL_AUTO)
+    vis_b, vis_f = ib == tg, i_f == tg
+    assert np.array_equal(vis_b, vis_f)
+    assert 0.05 < vis_f.mean() < 0.95
+    assert np.array_equal(bits(tb[vis_b]), bits(tf[vis_f]))
+
+
+def test_bvh_renders_equal_brute_force_and_oracle(oracle):
+    """Forward samples, adjoint and graph of the clutter scene (3 objects,
+    2 spheres): BVH == brute force bit-for-bit, and == the oracle."""
+    from inverse_path_tracer_amd import _native as N
+    from test_bvh import CLUTTER_SCENE
+
+    P = _bvh_scene(CLUTTER_SCENE)
+    Q = oracle.OracleScene(CLUTTER_SCENE)
+    W, H, spp, mb, seed = 48, 40, 4, 4, 77
+    got = P.render_samples(W, H, spp, mb, seed)
+    want, _ = Q.render_samples(W, H, spp, mb, seed)
+    assert np.array_equal(bits(got), bits(want))
+    P.set_accel(N.ACCEL_BRUTE)
+    big_f = P.render_samples(160, 128, 8, 4, 5)
+    P.set_accel(N.ACCEL_BVH)
+    big_b = P.render_samples(160, 128, 8, 4, 5)
+    assert np.array_equal(bits(big_f), bits(big_b))
+    adj = np.random.RandomState(3).uniform(-1, 1, (H, W, 3)).astype(np.float32)
+    np.testing.assert_allclose(P.adjoint(adj, W, H, spp, mb, seed), Q.adjoint(W, H, spp, mb, seed, adj),
+                               rtol=1e-9, atol=1e-12)
+    P.set_accel(N.ACCEL_AUTO)
