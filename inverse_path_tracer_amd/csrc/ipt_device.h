@@ -492,6 +492,12 @@ struct BvhView {
 };
 constexpr int kStackStride = 256;  // = the megakernel's block size
 constexpr int kBvhDone = (int)0x80000000;
+// Profiling build (make variant DEFS=-DIPT_BVH_STATS): casts, inner-node
+// visits, leaf pair tests and shadow early-outs, summed over all lanes
+// (ipt_debug_bvh_stats) -- the "tests actually executed" of the roofline.
+#ifdef IPT_BVH_STATS
+__device__ unsigned long long g_bvh_stats[4];
+#endif
 
 __device__ __forceinline__ void bvh_load_node(const BvhView &B, int n, float4 &q0, float4 &q1, float4 &q2,
                                               float4 &q3) {
@@ -573,8 +579,14 @@ __device__ __forceinline__ int closest_hit_bvh(const BvhView &B, V3 p, V3 d, flo
   uint32_t *stk = B.stack;
   int sp = 0;
   int node = 0;
+#ifdef IPT_BVH_STATS
+  uint32_t st_nodes = 0, st_pairs = 0;
+#endif
   while (node != kBvhDone) {
     while (node >= 0) {  // inner node: test both children's boxes
+#ifdef IPT_BVH_STATS
+      ++st_nodes;
+#endif
       float4 q0, q1, q2, q3;
       bvh_load_node(B, node, q0, q1, q2, q3);
       const f2 tx0 = fma2(f2{q0.x, q1.z}, ix2, ox2), tx1 = fma2(f2{q0.y, q1.w}, ix2, ox2);
@@ -601,10 +613,19 @@ __device__ __forceinline__ int closest_hit_bvh(const BvhView &B, V3 p, V3 d, flo
       const int code = ~node;
       const int first = code >> kBvhLeafPairBits, np = (code & ((1 << kBvhLeafPairBits) - 1)) + 1;
       for (int j = 0; j < np; ++j) bvh_pair_test(B.pairs[first + j], p, d, bt, bi);
+#ifdef IPT_BVH_STATS
+      st_pairs += np;
+#endif
       node = sp > 0 ? (int)stk[--sp * kStackStride] : kBvhDone;
       if (SHADOW && bi != target) node = kBvhDone;  // occluded: decided
     }
   }
+#ifdef IPT_BVH_STATS
+  atomicAdd(&g_bvh_stats[0], 1ull);
+  atomicAdd(&g_bvh_stats[1], (unsigned long long)st_nodes);
+  atomicAdd(&g_bvh_stats[2], (unsigned long long)st_pairs);
+  if (SHADOW && bi != target) atomicAdd(&g_bvh_stats[3], 1ull);
+#endif
   best_t = bt;
   return bi;
 }

@@ -102,7 +102,13 @@ struct TraceArgs {
   // BVH (BVH instances only): nodes staged in LDS (0: read from global),
   // traversal stack entries per lane
   int bvh_lds_nodes, bvh_stack;
-  int lds_grad;  // ADJ: gradient bins in LDS (else global fp64 atomics)
+  // ADJ gradient bins: grad_slots triangles accumulate in LDS fp64 (all of
+  // them when they fit, else the largest -- the most-hit -- ones, mapped by
+  // grad_map[tri] -> slot or -1, slot_tri[slot] -> tri); the rest go to
+  // global fp64 atomics directly
+  int grad_slots;
+  const int *grad_map;
+  const int *slot_tri;
   float cam[16];
 };
 
@@ -204,7 +210,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   double *lds_acc = lds;               // ADJ: nT*3 grad; GRAPH: (nT+1)*nT*kEdgeW bins
   int n_acc = 0;
   if (MODE == MODE_ADJ) {
-    n_acc = a.lds_grad ? nT * 3 : 0;
+    n_acc = a.grad_slots * 3;
   } else if (MODE == MODE_GRAPH && a.lds_edges) {
     n_acc = (nT + 1) * nT * kEdgeW;
   }
@@ -257,7 +263,6 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   for (int i = tid; i < n_acc; i += kBlock) lds_acc[i] = 0.0;
   __syncthreads();
   double *acc = (MODE == MODE_GRAPH && !a.lds_edges) ? edges : lds_acc;
-  double *gacc = (MODE == MODE_ADJ && !a.lds_grad) ? grad : lds_acc;  // ADJ gradient bins
 
   // wave-uniform sample range (static partition, regenerated per lane)
   const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * kBlock + tid) >> 6);
@@ -630,9 +635,13 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
               const float cpi = ck / kPiF;
               gk = mk(gk.x + (cpi * Mk.x) * S.x, gk.y + (cpi * Mk.y) * S.y, gk.z + (cpi * Mk.z) * S.z);
             }
-            atomicAdd(&gacc[tk * 3 + 0], (double)(ax * gk.x));
-            atomicAdd(&gacc[tk * 3 + 1], (double)(ay * gk.y));
-            atomicAdd(&gacc[tk * 3 + 2], (double)(az * gk.z));
+            {
+              const int sl = a.grad_map ? a.grad_map[tk] : tk;
+              double *gb = sl >= 0 ? lds_acc + sl * 3 : grad + tk * 3;
+              atomicAdd(gb + 0, (double)(ax * gk.x));
+              atomicAdd(gb + 1, (double)(ay * gk.y));
+              atomicAdd(gb + 2, (double)(az * gk.z));
+            }
             float dx, dy, dz, tx, ty, tz;
             ddir(tk, sdk, dx, dy, dz);
             tdiff(tk, si, tx, ty, tz);
@@ -655,7 +664,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       double *dstp = (MODE == MODE_ADJ) ? grad : edges;
       for (int i = tid; i < n_acc; i += kBlock) {
         const double v = lds_acc[i];
-        if (v != 0.0) atomicAdd(dstp + i, v);
+        const int j = (MODE == MODE_ADJ && a.slot_tri) ? a.slot_tri[i / 3] * 3 + i % 3 : i;
+        if (v != 0.0) atomicAdd(dstp + j, v);
       }
     }
   }
@@ -729,6 +739,7 @@ struct GpuScene {
   BvhNode *bnodes = nullptr;
   BvhPair *bpairs = nullptr;
   int accel = IPT_ACCEL_AUTO;
+  int *grad_map = nullptr, *slot_tri = nullptr;  // ADJ hot-set LDS slots (large scenes)
   int grid[12] = {0};       // resident workgroups per (mode, spec, bvh) (0 = not queried)
   size_t grid_lds[12] = {0};
 };
@@ -738,6 +749,14 @@ extern "C" int ipt_debug_phase_cycles(unsigned long long *out) {  // read and re
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
   unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#endif
+
+#ifdef IPT_BVH_STATS
+extern "C" int ipt_debug_bvh_stats(unsigned long long *out) {  // read and reset (4 counters)
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bvh_stats), 4 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  unsigned long long z[4] = {0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_bvh_stats), z, sizeof z) == hipSuccess ? 0 : -1;
 }
 #endif
 
@@ -770,6 +789,24 @@ GpuScene *gpu_upload(const HostScene &host, std::string *err) {
     return nullptr;
   }
   for (const TriMat &m : host.mat) s->has_ks |= (m.flags & MAT_HAS_KS) != 0;
+  if ((size_t)host.nT * 3 * sizeof(double) > (size_t)kLdsGradBytes) {
+    // adjoint gradient bins: the largest triangles (most path vertices land on
+    // them, so their bins are the contended ones) get LDS slots
+    const int slots = kLdsGradBytes / (3 * (int)sizeof(double));
+    std::vector<int> order(host.nT), map(host.nT, -1), inv(slots);
+    for (int i = 0; i < host.nT; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int x, int y) { return host.geom[(size_t)x].area > host.geom[(size_t)y].area; });
+    for (int k = 0; k < slots; ++k) {
+      map[(size_t)order[(size_t)k]] = k;
+      inv[(size_t)k] = order[(size_t)k];
+    }
+    if (upload(&s->grad_map, map) || upload(&s->slot_tri, inv)) {
+      *err = gpu_last_error();
+      gpu_free(s);
+      return nullptr;
+    }
+  }
   s->on_device = true;
   return s;
 }
@@ -798,6 +835,8 @@ void gpu_free(GpuScene *s) {
   (void)hipFree(s->ws);
   (void)hipFree(s->bnodes);
   (void)hipFree(s->bpairs);
+  (void)hipFree(s->grad_map);
+  (void)hipFree(s->slot_tri);
   delete s;
 }
 
@@ -880,7 +919,9 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.m_npix = a.npix > 1 ? ~0ull / a.npix + 1 : 0;
   a.bvh_lds_nodes = 0;
   a.bvh_stack = 0;
-  a.lds_grad = 1;
+  a.grad_slots = 0;
+  a.grad_map = nullptr;
+  a.slot_tri = nullptr;
   std::memcpy(a.cam, s->host.cam, sizeof a.cam);
   return a;
 }
@@ -1008,8 +1049,14 @@ int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const f
     return -1;
   }
   TraceArgs a = make_args(s, p);
-  a.lds_grad = (size_t)s->host.nT * 3 * sizeof(double) <= (size_t)kLdsGradBytes ? 1 : 0;
-  const size_t lds = (a.lds_grad ? (size_t)s->host.nT * 3 * sizeof(double) : 0) + table_bytes(a) +
+  if (s->grad_map) {
+    a.grad_slots = kLdsGradBytes / (3 * (int)sizeof(double));
+    a.grad_map = s->grad_map;
+    a.slot_tri = s->slot_tri;
+  } else {
+    a.grad_slots = s->host.nT;
+  }
+  const size_t lds = (size_t)a.grad_slots * 3 * sizeof(double) + table_bytes(a) +
                      (size_t)(p.max_bounces + 1) * (s->has_ks ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock *
                          sizeof(float);
   if (lds > 160 * 1024) {
