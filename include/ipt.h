@@ -109,12 +109,15 @@ int ipt_scene_camera(void *scene, float *out16);
 #define IPT_ACCEL_BRUTE 1
 #define IPT_ACCEL_BVH 2
 int ipt_scene_set_accel(void *scene, int mode);
-/* info4 = {nodes, leaf pairs, depth, accel in use (IPT_ACCEL_BRUTE/BVH)};
- * returns 1 if the scene has a BVH, 0 if not (ipt_last_error says why). */
-int ipt_scene_bvh_info(void *scene, int32_t *info4);
-/* nodes: info4[0]*16 floats (BvhNode), pairs: info4[1]*40 floats (BvhPair:
- * 18 field pairs, then 2 int32 triangle indices, 2 pad); either nullable. */
-int ipt_scene_export_bvh(void *scene, float *nodes, float *pairs);
+/* info8 = {nodes, leaf pairs, depth, accel in use (IPT_ACCEL_BRUTE/BVH),
+ * large-triangle pairs tested before the traversal, 0, 0, 0}; returns 1 if
+ * the scene has a BVH, 0 if not (ipt_last_error says why). */
+int ipt_scene_bvh_info(void *scene, int32_t *info8);
+/* nodes: info8[0]*16 floats (BvhNode), pairs: info8[1]*40 floats (BvhPair:
+ * 18 field pairs, then 2 int32 triangle indices, 2 pad), big_idx:
+ * info8[4]*2 int32 (the pre-pass triangles, 0x7fffffff = padding); each
+ * nullable. */
+int ipt_scene_export_bvh(void *scene, float *nodes, float *pairs, int32_t *big_idx);
 /* Closest hit of n rays (origins, dirs: n*3 floats) through the kernels'
  * own cast: idx = triangle index or -1, t = its distance.  targets
  * (nullable, n ints): >= 0 marks a next-event shadow ray towards that

@@ -46,6 +46,12 @@ namespace {
 constexpr int kBins = 32;
 constexpr int kMaxLeafTris = 8;  // SAH may stop at <= 8 triangles (4 pairs)
 constexpr double kCostNode = 1.0, kCostPair = 1.0;
+// Triangles whose acceptance box has at least this fraction of the scene
+// box's surface area (almost every ray reaches them: room walls) are tested
+// by the unrolled brute-force pair loop ahead of the traversal, up to 2 *
+// kBigPairs of them, instead of sitting in leaves that every ray visits.
+constexpr double kBigFrac = 1.0 / 32;
+constexpr int kBigPairs = 16;  // = ipt_device.h kSmallPairs
 
 struct Box {
   float lo[3] = {std::numeric_limits<float>::infinity(), std::numeric_limits<float>::infinity(),
@@ -285,6 +291,8 @@ int acceptance_box(const TriIsect &T, const TriGeom &G, double r_all, float lo[3
 bool build_bvh(HostScene *S) {
   S->bvh_nodes.clear();
   S->bvh_pairs.clear();
+  S->bvh_big_pairs.clear();
+  S->bvh_big_idx.clear();
   S->bvh_depth = 0;
   const double r_all = scene_coord_bound(*S);
   Builder B;
@@ -300,8 +308,43 @@ bool build_bvh(HostScene *S) {
     p.tri = i;
     B.prims.push_back(p);
   }
+  // the large triangles go to the brute-force pre-pass
+  {
+    Box all;
+    for (const Prim &p : B.prims) all.grow(p.box);
+    const double lim = kBigFrac * all.area();
+    std::vector<size_t> cand;
+    for (size_t k = 0; k < B.prims.size(); ++k)
+      if (B.prims[k].box.area() >= lim) cand.push_back(k);
+    std::stable_sort(cand.begin(), cand.end(),
+                     [&](size_t x, size_t y) { return B.prims[x].box.area() > B.prims[y].box.area(); });
+    if (cand.size() > (size_t)(2 * kBigPairs)) cand.resize(2 * kBigPairs);
+    std::vector<int> big;
+    std::vector<char> drop(B.prims.size(), 0);
+    for (size_t k : cand) {
+      big.push_back(B.prims[k].tri);
+      drop[k] = 1;
+    }
+    std::sort(big.begin(), big.end());
+    std::vector<Prim> rest;
+    for (size_t k = 0; k < B.prims.size(); ++k)
+      if (!drop[k]) rest.push_back(B.prims[k]);
+    B.prims.swap(rest);
+    const int np = ((int)big.size() + 1) / 2;
+    S->bvh_big_pairs.assign((size_t)np, TriPair());
+    S->bvh_big_idx.assign((size_t)np * 2, 0x7fffffff);
+    std::vector<TriIsect> recs((size_t)np * 2);
+    for (auto &r : recs) std::memset(&r, 0, sizeof r);
+    for (size_t k = 0; k < big.size(); ++k) {
+      recs[k] = S->isect[(size_t)big[k]];
+      S->bvh_big_idx[k] = big[k];
+    }
+    if (np > 0) pack_pairs(recs.data(), 2 * np, S->bvh_big_pairs.data());
+  }
   if (B.prims.size() < 2) {
-    S->bvh_status = "fewer than two hittable triangles";
+    S->bvh_status = "fewer than two hittable triangles outside the brute-force set";
+    S->bvh_big_pairs.clear();
+    S->bvh_big_idx.clear();
     return false;
   }
   Box root_box;

@@ -188,21 +188,25 @@ int ipt_scene_camera(void *scene, float *out16) {
   return 0;
 }
 
-int ipt_scene_bvh_info(void *scene, int32_t *info4) {
+int ipt_scene_bvh_info(void *scene, int32_t *info8) {
   GpuScene *s = as_scene(scene);
-  if (!s || !info4) return -1;
+  if (!s || !info8) return -1;
   const ipt::HostScene &h = ipt::gpu_host(s);
-  info4[0] = (int32_t)h.bvh_nodes.size();
-  info4[1] = (int32_t)h.bvh_pairs.size();
-  info4[2] = h.bvh_depth;
-  info4[3] = ipt::gpu_accel_in_use(s);
+  info8[0] = (int32_t)h.bvh_nodes.size();
+  info8[1] = (int32_t)h.bvh_pairs.size();
+  info8[2] = h.bvh_depth;
+  info8[3] = ipt::gpu_accel_in_use(s);
+  info8[4] = (int32_t)h.bvh_big_pairs.size();
+  info8[5] = info8[6] = info8[7] = 0;
   if (h.bvh_nodes.empty()) fail("no BVH: " + h.bvh_status);
   return h.bvh_nodes.empty() ? 0 : 1;
 }
-int ipt_scene_export_bvh(void *scene, float *nodes, float *pairs) {
+int ipt_scene_export_bvh(void *scene, float *nodes, float *pairs, int32_t *big_idx) {
   GpuScene *s = as_scene(scene);
   if (!s) return -1;
   const ipt::HostScene &h = ipt::gpu_host(s);
+  if (big_idx && !h.bvh_big_idx.empty())
+    std::memcpy(big_idx, h.bvh_big_idx.data(), h.bvh_big_idx.size() * sizeof(int32_t));
   if (nodes && !h.bvh_nodes.empty()) std::memcpy(nodes, h.bvh_nodes.data(), h.bvh_nodes.size() * sizeof(ipt::BvhNode));
   if (pairs && !h.bvh_pairs.empty()) std::memcpy(pairs, h.bvh_pairs.data(), h.bvh_pairs.size() * sizeof(ipt::BvhPair));
   return 0;

@@ -388,7 +388,11 @@ __device__ __forceinline__ PairOrigin pair_origin(const TriPair &T, V3 p) {
   o.num = fma2(o.pz, n2, fma2(o.py, n1, o.px * n0));
   return o;
 }
-__device__ __forceinline__ void pair_ray(const TriPair &T, const PairOrigin &o, int i, V3 p, V3 d, float &bt,
+// LEX = false: the reference's in-order strict '<' (triangles ia < ib come in
+// index order).  LEX = true: keep the lexicographic minimum of (t, index) --
+// the same result whatever order the triangles are visited in (BVH scenes).
+template <bool LEX = false>
+__device__ __forceinline__ void pair_ray(const TriPair &T, const PairOrigin &o, int ia, int ib, V3 p, V3 d, float &bt,
                                          int &bi, f2 e03, f2 e13, f2 e23) {
   const f2 n0 = ld2(T, 3), n1 = ld2(T, 4), n2 = ld2(T, 5);
   const f2 denom = fma2(n2, bc2(d.z), fma2(n1, bc2(d.y), n0 * bc2(d.x)));
@@ -411,17 +415,30 @@ __device__ __forceinline__ void pair_ray(const TriPair &T, const PairOrigin &o, 
   const f2 s0 = fma2(qz, ld2(T, 8), fma2(qy, ld2(T, 7), fma2(qx, ld2(T, 6), e03)));
   const f2 s1 = fma2(qz, ld2(T, 12), fma2(qy, ld2(T, 11), fma2(qx, ld2(T, 10), e13)));
   const f2 s2 = fma2(qz, ld2(T, 16), fma2(qy, ld2(T, 15), fma2(qx, ld2(T, 14), e23)));
+  if (LEX) {
+    const bool va = !(fabsf(denom.x) < kMinDotUp) && !(t.x < kEpsUp) && !(s0.x > 0.f) && !(s1.x > 0.f) &&
+                    !(s2.x > 0.f);
+    const bool ta = va && (t.x < bt || (t.x == bt && ia < bi));
+    bt = ta ? t.x : bt;
+    bi = ta ? ia : bi;
+    const bool vb = !(fabsf(denom.y) < kMinDotUp) && !(t.y < kEpsUp) && !(s0.y > 0.f) && !(s1.y > 0.f) &&
+                    !(s2.y > 0.f);
+    const bool tb = vb && (t.y < bt || (t.y == bt && ib < bi));
+    bt = tb ? t.y : bt;
+    bi = tb ? ib : bi;
+    return;
+  }
   const bool ta = !(fabsf(denom.x) < kMinDotUp) && !(t.x < kEpsUp) && !(t.x >= bt) && !(s0.x > 0.f) &&
                   !(s1.x > 0.f) && !(s2.x > 0.f);
   bt = ta ? t.x : bt;
-  bi = ta ? i : bi;
+  bi = ta ? ia : bi;
   const bool tb = !(fabsf(denom.y) < kMinDotUp) && !(t.y < kEpsUp) && !(t.y >= bt) && !(s0.y > 0.f) &&
                   !(s1.y > 0.f) && !(s2.y > 0.f);
   bt = tb ? t.y : bt;
-  bi = tb ? i + 1 : bi;
+  bi = tb ? ib : bi;
 }
 __device__ __forceinline__ void hit_test_pair(const TriPair &T, int i, V3 p, V3 d, float &bt, int &bi) {
-  pair_ray(T, pair_origin(T, p), i, p, d, bt, bi, ld2(T, 9), ld2(T, 13), ld2(T, 17));
+  pair_ray(T, pair_origin(T, p), i, i + 1, p, d, bt, bi, ld2(T, 9), ld2(T, 13), ld2(T, 17));
 }
 
 // Small scenes (nT <= 2 * kSmallPairs): the pair loop fully unrolled, and the
@@ -443,7 +460,7 @@ __device__ __forceinline__ int closest_hit_pairs_small(const TriPair *__restrict
   for (int j = 0; j < kSmallPairs; ++j) {
     if (j < nP) {  // wave-uniform
       const TriPair T = pairs[j];
-      pair_ray(T, pair_origin(T, p), 2 * j, p, d, bt, bi, e3[3 * j], e3[3 * j + 1], e3[3 * j + 2]);
+      pair_ray(T, pair_origin(T, p), 2 * j, 2 * j + 1, p, d, bt, bi, e3[3 * j], e3[3 * j + 1], e3[3 * j + 2]);
     }
   }
   best_t = bt;
@@ -489,6 +506,11 @@ struct BvhView {
   const BvhPair *pairs;
   const TriIsect *isect;    // original-order records (shadow target test)
   uint32_t *stack;          // LDS, entry k of this lane at stack[k * kStride]
+  // brute-force pre-pass over the large triangles (bvh.cpp kBigFrac)
+  const TriPair *big;
+  const int32_t *big_idx;   // original indices, 2 per pair
+  const f2 *big_e3;         // LDS: the pairs' edge-plane offsets
+  int nbig;                 // pairs (<= kSmallPairs)
 };
 constexpr int kStackStride = 256;  // = the megakernel's block size
 constexpr int kBvhDone = (int)0x80000000;
@@ -549,6 +571,21 @@ __device__ __forceinline__ void bvh_pair_test(const BvhPair &T, V3 p, V3 d, floa
   bi = tb ? T.idx[1] : bi;
 }
 
+// The large triangles, unrolled like closest_hit_pairs_small (scalar-loaded
+// pairs, plane offsets from LDS) with the lexicographic accept.
+__device__ __forceinline__ void bvh_big_pass(const BvhView &B, V3 p, V3 d, float &bt, int &bi) {
+  int nP = B.nbig;
+  asm volatile("" : "+s"(nP));
+#pragma unroll
+  for (int j = 0; j < kSmallPairs; ++j) {
+    if (j < nP) {  // wave-uniform
+      const TriPair T = B.big[j];
+      pair_ray<true>(T, pair_origin(T, p), B.big_idx[2 * j], B.big_idx[2 * j + 1], p, d, bt, bi, B.big_e3[3 * j],
+                     B.big_e3[3 * j + 1], B.big_e3[3 * j + 2]);
+    }
+  }
+}
+
 // Closest hit through the BVH.  target < 0: ordinary cast.  target >= 0
 // (next-event shadow ray towards emitter triangle `target`): the caller only
 // needs to know whether the closest hit IS `target` (and its t), so the
@@ -565,6 +602,13 @@ __device__ __forceinline__ int closest_hit_bvh(const BvhView &B, V3 p, V3 d, flo
     if (bi < 0) {
       best_t = bt;
       return -1;  // the target itself is missed: not the closest hit either
+    }
+  }
+  if (B.nbig > 0) {
+    bvh_big_pass(B, p, d, bt, bi);
+    if (SHADOW && bi != target) {  // occluded by a large triangle: decided
+      best_t = bt;
+      return bi;
     }
   }
   // slab parameters t = fma(box, 1/d, -p/d); |d| < 2^-60: slab ignored (NaN)

@@ -102,6 +102,9 @@ struct TraceArgs {
   // BVH (BVH instances only): nodes staged in LDS (0: read from global),
   // traversal stack entries per lane
   int bvh_lds_nodes, bvh_stack;
+  int bvh_nbig;                 // large-triangle pairs tested before the traversal
+  const TriPair *bvh_big;
+  const int32_t *bvh_big_idx;
   // ADJ gradient bins: grad_slots triangles accumulate in LDS fp64 (all of
   // them when they fit, else the largest -- the most-hit -- ones, mapped by
   // grad_map[tri] -> slot or -1, slot_tri[slot] -> tri); the rest go to
@@ -248,6 +251,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   bv.isect = isect;
   bv.lnodes = nullptr;
   bv.stack = nullptr;
+  bv.big = nullptr;
+  bv.big_idx = nullptr;
+  bv.big_e3 = nullptr;
+  bv.nbig = 0;
   if (BVH) {
     const size_t rec_words = (MODE == MODE_ADJ) ? (size_t)vmax * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock : 0;
     char *base = reinterpret_cast<char *>(lds);
@@ -258,7 +265,16 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       for (int i = tid; i < 4 * a.bvh_lds_nodes; i += kBlock) ln[i] = g[i];
       bv.lnodes = ln;
     }
-    bv.stack = reinterpret_cast<uint32_t *>(ln + 4 * a.bvh_lds_nodes) + tid;
+    float *be3 = reinterpret_cast<float *>(ln + 4 * a.bvh_lds_nodes);
+    for (int i = tid; i < 6 * a.bvh_nbig; i += kBlock) {
+      const int j = i / 6, kf = (i % 6) >> 1, h = i & 1;
+      be3[i] = a.bvh_big[j].f[9 + 4 * kf][h];
+    }
+    bv.big = a.bvh_big;
+    bv.big_idx = a.bvh_big_idx;
+    bv.big_e3 = reinterpret_cast<const f2 *>(be3);
+    bv.nbig = a.bvh_nbig;
+    bv.stack = reinterpret_cast<uint32_t *>(be3 + 6 * a.bvh_nbig) + tid;
   }
   for (int i = tid; i < n_acc; i += kBlock) lds_acc[i] = 0.0;
   __syncthreads();
@@ -738,6 +754,8 @@ struct GpuScene {
   bool has_ks = false;      // some material has a Phong lobe
   BvhNode *bnodes = nullptr;
   BvhPair *bpairs = nullptr;
+  TriPair *big_pairs = nullptr;
+  int32_t *big_idx = nullptr;
   int accel = IPT_ACCEL_AUTO;
   int *grad_map = nullptr, *slot_tri = nullptr;  // ADJ hot-set LDS slots (large scenes)
   int grid[12] = {0};       // resident workgroups per (mode, spec, bvh) (0 = not queried)
@@ -783,7 +801,8 @@ GpuScene *gpu_upload(const HostScene &host, std::string *err) {
   pack_pairs(host.isect.data(), (int)host.isect.size(), pairs.data());
   if (upload(&s->isect, host.isect) || upload(&s->pairs, pairs) || upload(&s->geom, host.geom) || upload(&s->mat, host.mat) ||
       upload(&s->kd, host.kd) || upload(&s->emit_tri, host.emit_tri) || upload(&s->emit_cdf, host.emit_cdf) ||
-      upload(&s->emit_pmf, host.emit_pmf) || upload(&s->bnodes, host.bvh_nodes) || upload(&s->bpairs, host.bvh_pairs)) {
+      upload(&s->emit_pmf, host.emit_pmf) || upload(&s->bnodes, host.bvh_nodes) || upload(&s->bpairs, host.bvh_pairs) ||
+      upload(&s->big_pairs, host.bvh_big_pairs) || upload(&s->big_idx, host.bvh_big_idx)) {
     *err = gpu_last_error();
     gpu_free(s);
     return nullptr;
@@ -835,6 +854,8 @@ void gpu_free(GpuScene *s) {
   (void)hipFree(s->ws);
   (void)hipFree(s->bnodes);
   (void)hipFree(s->bpairs);
+  (void)hipFree(s->big_pairs);
+  (void)hipFree(s->big_idx);
   (void)hipFree(s->grad_map);
   (void)hipFree(s->slot_tri);
   delete s;
@@ -919,6 +940,9 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.m_npix = a.npix > 1 ? ~0ull / a.npix + 1 : 0;
   a.bvh_lds_nodes = 0;
   a.bvh_stack = 0;
+  a.bvh_nbig = 0;
+  a.bvh_big = nullptr;
+  a.bvh_big_idx = nullptr;
   a.grad_slots = 0;
   a.grad_map = nullptr;
   a.slot_tri = nullptr;
@@ -940,7 +964,10 @@ static size_t bvh_lds(const GpuScene *s, TraceArgs &a, size_t base) {
   const size_t nn = s->host.bvh_nodes.size();
   a.bvh_lds_nodes = nn * sizeof(BvhNode) <= (size_t)kBvhLdsNodeBytes ? (int)nn : 0;
   a.bvh_stack = std::max(1, s->host.bvh_depth);
-  return bvh_lds_offset(base) + (size_t)a.bvh_lds_nodes * sizeof(BvhNode) +
+  a.bvh_nbig = (int)s->host.bvh_big_pairs.size();
+  a.bvh_big = s->big_pairs;
+  a.bvh_big_idx = s->big_idx;
+  return bvh_lds_offset(base) + (size_t)a.bvh_lds_nodes * sizeof(BvhNode) + (size_t)a.bvh_nbig * 6 * sizeof(float) +
          (size_t)a.bvh_stack * kBlock * sizeof(uint32_t);
 }
 
@@ -1196,7 +1223,9 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
                                                              const TriPair *__restrict__ pairs,
                                                              const BvhNode *__restrict__ bnodes,
                                                              const BvhPair *__restrict__ bpairs, int nT, int small,
-                                                             int lds_nodes, int64_t n, const float *__restrict__ org,
+                                                             int lds_nodes, const TriPair *__restrict__ big,
+                                                             const int32_t *__restrict__ big_idx, int nbig, int64_t n,
+                                                             const float *__restrict__ org,
                                                              const float *__restrict__ dir,
                                                              const int *__restrict__ targets, float *__restrict__ t_out,
                                                              int *__restrict__ i_out) {
@@ -1218,6 +1247,10 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
   bv.isect = isect;
   bv.lnodes = nullptr;
   bv.stack = nullptr;
+  bv.big = nullptr;
+  bv.big_idx = nullptr;
+  bv.big_e3 = nullptr;
+  bv.nbig = 0;
   if (BVH) {
     char *base = reinterpret_cast<char *>(lds);
     float4 *ln = reinterpret_cast<float4 *>(base + bvh_lds_offset((size_t)(small ? 6 * nP : 0) * sizeof(float)));
@@ -1226,7 +1259,16 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
       for (int i = tid; i < 4 * lds_nodes; i += kBlock) ln[i] = g[i];
       bv.lnodes = ln;
     }
-    bv.stack = reinterpret_cast<uint32_t *>(ln + 4 * lds_nodes) + tid;
+    float *be3 = reinterpret_cast<float *>(ln + 4 * lds_nodes);
+    for (int i = tid; i < 6 * nbig; i += kBlock) {
+      const int j = i / 6, kf = (i % 6) >> 1, h = i & 1;
+      be3[i] = big[j].f[9 + 4 * kf][h];
+    }
+    bv.big = big;
+    bv.big_idx = big_idx;
+    bv.big_e3 = reinterpret_cast<const f2 *>(be3);
+    bv.nbig = nbig;
+    bv.stack = reinterpret_cast<uint32_t *>(be3 + 6 * nbig) + tid;
   }
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * kBlock + tid;
@@ -1270,12 +1312,12 @@ int gpu_closest_hit(GpuScene *s, int64_t n, const float *org_dev, const float *d
   if (use_bvh(s)) {
     const size_t lds = bvh_lds(s, a, base);
     hipLaunchKernelGGL(closest_hit_kernel<true>, dim3(blocks), dim3(kBlock), lds, (hipStream_t)stream, s->isect,
-                       s->pairs, s->bnodes, s->bpairs, s->host.nT, small, a.bvh_lds_nodes, n, org_dev, dir_dev,
-                       targets_dev, t_dev, idx_dev);
+                       s->pairs, s->bnodes, s->bpairs, s->host.nT, small, a.bvh_lds_nodes, a.bvh_big, a.bvh_big_idx,
+                       a.bvh_nbig, n, org_dev, dir_dev, targets_dev, t_dev, idx_dev);
   } else {
     hipLaunchKernelGGL(closest_hit_kernel<false>, dim3(blocks), dim3(kBlock), base, (hipStream_t)stream, s->isect,
-                       s->pairs, s->bnodes, s->bpairs, s->host.nT, small, 0, n, org_dev, dir_dev, targets_dev, t_dev,
-                       idx_dev);
+                       s->pairs, s->bnodes, s->bpairs, s->host.nT, small, 0, nullptr, nullptr, 0, n, org_dev, dir_dev,
+                       targets_dev, t_dev, idx_dev);
   }
   HIP_TRY(hipGetLastError());
   return 0;

@@ -31,6 +31,11 @@ struct HostScene {
   std::vector<BvhNode> bvh_nodes;
   std::vector<BvhPair> bvh_pairs;
   int bvh_depth = 0;           // inner-node levels (stack entries needed)
+  // triangles tested by the unrolled brute-force pair loop before the BVH
+  // (the few large ones, e.g. Cornell walls, that almost every ray reaches):
+  // pairs in ascending original index, padded with zero triangles
+  std::vector<TriPair> bvh_big_pairs;
+  std::vector<int32_t> bvh_big_idx;  // 2 per pair; 0x7fffffff = padding
   std::string bvh_status;      // "ok" or why the BVH was not built
 };
 

@@ -151,22 +151,24 @@ class Scene:
         N.check(N.lib().ipt_scene_set_accel(self.handle, int(mode)), "set_accel")
 
     def bvh_info(self) -> dict:
-        info = (C.c_int32 * 4)()
+        info = (C.c_int32 * 8)()
         has = N.lib().ipt_scene_bvh_info(self.handle, info)
         N.check(has, "bvh_info")
-        return {"has_bvh": bool(has), "nodes": info[0], "pairs": info[1], "depth": info[2],
+        return {"has_bvh": bool(has), "nodes": info[0], "pairs": info[1], "depth": info[2], "big_pairs": info[4],
                 "accel": {N.ACCEL_BRUTE: "brute", N.ACCEL_BVH: "bvh"}.get(info[3], "?"),
                 "status": "ok" if has else N.last_error()}
 
     def export_bvh(self):
-        """(nodes[n,16] float32, pairs[m,40] float32) -- BvhNode / BvhPair
-        records (scene_layout.h); child links and indices are int32 bits."""
+        """(nodes[n,16] float32, pairs[m,40] float32, big_idx[2k] int32) --
+        BvhNode / BvhPair records (scene_layout.h; child links and indices are
+        int32 bits) and the large triangles tested before the traversal."""
         i = self.bvh_info()
         nodes = np.zeros((i["nodes"], 16), np.float32)
         pairs = np.zeros((i["pairs"], 40), np.float32)
-        N.check(N.lib().ipt_scene_export_bvh(self.handle, nodes.ctypes.data_as(N.fp), pairs.ctypes.data_as(N.fp)),
-                "export_bvh")
-        return nodes, pairs
+        big = np.zeros(2 * i["big_pairs"], np.int32)
+        N.check(N.lib().ipt_scene_export_bvh(self.handle, nodes.ctypes.data_as(N.fp), pairs.ctypes.data_as(N.fp),
+                                             big.ctypes.data_as(C.POINTER(C.c_int32))), "export_bvh")
+        return nodes, pairs, big
 
     def closest_hit(self, origins, dirs, targets=None):
         """The kernels' cast on caller rays: (t float32[n], idx int32[n])."""

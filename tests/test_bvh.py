@@ -61,9 +61,12 @@ def test_bvh_selected_by_size():
 @pytest.mark.parametrize("recs", [SPHERE_SCENE, CLUTTER_SCENE], ids=["sphere", "clutter"])
 def test_bvh_structure(recs):
     P = product_scene(recs, device=False)
-    nodes, pairs = P.export_bvh()
+    nodes, pairs, big = P.export_bvh()
     kids, parent, leaves = _tree(nodes)
     idx = np.ascontiguousarray(pairs[:, 36:38]).view(np.int32)
+    # the Cornell walls and light (18 large triangles) are the brute-force pre-pass
+    bigr = big[big != 0x7FFFFFFF]
+    assert sorted(bigr.tolist()) == list(range(18)) and np.all(np.diff(bigr) > 0)
     # breadth-first numbering: children come after their parent
     for n in range(len(nodes)):
         for c in range(2):
@@ -76,7 +79,7 @@ def test_bvh_structure(recs):
         covered[first:first + npairs] += 1
     assert np.all(covered == 1)
     real = idx[idx != 0x7FFFFFFF]
-    assert sorted(real.tolist()) == list(range(P.nT))
+    assert sorted(real.tolist() + bigr.tolist()) == list(range(P.nT))
     pad = idx == 0x7FFFFFFF
     assert np.all(pairs[:, :36].reshape(-1, 18, 2)[pad.nonzero()[0], :, pad.nonzero()[1]] == 0)
     # a child's box lies inside the box its parent stores for it
@@ -151,8 +154,9 @@ def test_acceptance_inside_every_ancestor_box(oracle, recs):
     tris = P.triangles()
     cam = P.camera()
     cam_origin = cam[:3, 3].astype(np.float64)
-    nodes, pairs = P.export_bvh()
+    nodes, pairs, big = P.export_bvh()
     _, parent, leaves = _tree(nodes)
+    bigset = set(big.tolist())
     idx = np.ascontiguousarray(pairs[:, 36:38]).view(np.int32)
     tri_slot = {}
     for first, npairs, pn, pc in leaves:
@@ -169,6 +173,8 @@ def test_acceptance_inside_every_ancestor_box(oracle, recs):
         for i in np.nonzero(~np.isnan(t))[0]:
             accepted += 1
             x = o.astype(np.float64) + float(t[i]) * d.astype(np.float64)
+            if int(i) in bigset:
+                continue  # tested by the brute-force pre-pass for every ray
             slot = tri_slot[int(i)]
             while slot is not None:
                 lo, hi = _box(nodes, *slot)
@@ -177,7 +183,7 @@ def test_acceptance_inside_every_ancestor_box(oracle, recs):
     assert accepted > 1000
 
 
-def _traverse(nodes, pairs, kids, o, d, oracle_scene):
+def _traverse(nodes, pairs, big, kids, o, d, oracle_scene):
     """float32 emulation of ipt_device.h::closest_hit_bvh (exact reciprocal
     instead of v_rcp_f32; the leaf test's t from the oracle's own test)."""
     f = np.float32
@@ -188,6 +194,9 @@ def _traverse(nodes, pairs, kids, o, d, oracle_scene):
     teach = oracle_scene.hit_each(o, d)
     idx = np.ascontiguousarray(pairs[:, 36:38]).view(np.int32)
     bt, bi = np.float32(np.inf), -1
+    for i in big:  # the pre-pass over the large triangles
+        if i != 0x7FFFFFFF and not np.isnan(teach[i]) and (teach[i] < bt or (teach[i] == bt and i < bi)):
+            bt, bi = teach[i], int(i)
     stack, node = [], 0
     while node is not None:
         while node is not None and node >= 0:
@@ -229,14 +238,14 @@ def _traverse(nodes, pairs, kids, o, d, oracle_scene):
 
 def test_emulated_traversal_matches_oracle_closest_hit(sphere_scene):
     P, Q = sphere_scene
-    nodes, pairs = P.export_bvh()
+    nodes, pairs, big = P.export_bvh()
     kids, _, _ = _tree(nodes)
     tris = P.triangles()
     cam_origin = P.camera()[:3, 3].astype(np.float64)
     O, D = _adversarial_rays(tris, cam_origin, np.random.RandomState(5), 400)
     t_ref, i_ref = Q.closest_hit(O, D)
     for k in range(len(O)):
-        bt, bi = _traverse(nodes, pairs, kids, O[k], D[k], Q)
+        bt, bi = _traverse(nodes, pairs, big, kids, O[k], D[k], Q)
         assert bi == i_ref[k], k
         if bi >= 0:
             assert np.float32(bt).view(np.uint32) == t_ref[k].view(np.uint32)
@@ -253,6 +262,7 @@ def test_never_hit_triangle_left_out(tmp_path):
     assert P.nT == 1299 and np.all(P.triangles()[1298, 18:21] == 0)
     info = P.bvh_info()
     assert info["has_bvh"] and info["accel"] == "bvh"
-    _, pairs = P.export_bvh()
+    _, pairs, big = P.export_bvh()
     idx = np.ascontiguousarray(pairs[:, 36:38]).view(np.int32)
-    assert 1298 not in idx and sorted(idx[idx != 0x7FFFFFFF].tolist()) == list(range(1298))
+    got = idx[idx != 0x7FFFFFFF].tolist() + big[big != 0x7FFFFFFF].tolist()
+    assert 1298 not in got and sorted(got) == list(range(1298))

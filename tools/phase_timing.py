@@ -28,7 +28,7 @@ def main():
         p = N.make_params(512, 512, 64, 4, 0)
         buf = torch.empty((512 * 512 * 64, 3), device=dev)
         adj = torch.ones((512, 512, 3), device=dev)
-        g = torch.zeros((64, 3), dtype=torch.float64, device=dev)
+        g = torch.zeros((8192, 3), dtype=torch.float64, device=dev)
         cyc = (C.c_ulonglong * 8)()
         for kind in ("fwd", "adj"):
             for rep in range(2):

@@ -20,6 +20,9 @@ SCENES = {
 }
 SCENES["scene0"] = SCENES["cornell"] + [(A + "/shapes/cube.obj", "*Kd 0.9041462985304743 0.5854651848798454 0.007022117649276849*",
                                           (0, -1.5, 4), (0, 0, 0), (1, 1, 1))]
+if os.environ.get("IPT_VB_SPHERE"):  # large scene: BVH instance (triangle BVH + large-triangle pre-pass)
+    SCENES["sphere"] = SCENES["cornell"] + [(A + "/shapes/sphere.obj", "*Kd 0.2 0.6 0.3*", (0.3, -1.2, 4.2), (0.0, 0.4, 0.0),
+                                             (1.2, 1.2, 1.2))]
 
 
 def load(path):
@@ -67,7 +70,7 @@ def main():
         p = N.make_params(512, 512, 64, 4, 0)
         buf = torch.empty((512 * 512 * 64, 3), device=dev)
         adj = torch.ones((512, 512, 3), device=dev)
-        g = torch.zeros((64, 3), dtype=torch.float64, device=dev)
+        g = torch.zeros((8192, 3), dtype=torch.float64, device=dev)
         kinds = ("fwd", "fsm", "adj")
         times = {n: {k: [] for k in kinds} for n in libs}
         for rnd in range(6):
