@@ -36,6 +36,13 @@ BOUNCES = 4
 ASSETS = os.path.join(ROOT, "assets")
 CORNELL = [ObjectSpec(os.path.join(ASSETS, "CornellBox", "CornellBox-Empty-CO.obj"),
                       os.path.join(ASSETS, "CornellBox", "CornellBox-Empty-CO.mtl"), (0, 0, 4), (0, 0, 0), (2, 2, 2))]
+# C3 (BASELINE.json configs[2]): scenes/0.txt = Cornell + the cube with its inline Kd
+SCENE0 = CORNELL + [ObjectSpec(os.path.join(ASSETS, "shapes", "cube.obj"),
+                               "*Kd 0.9041462985304743 0.5854651848798454 0.007022117649276849*", (0, -1.5, 4),
+                               (0, 0, 0), (1, 1, 1))]
+# the north_star's "+ sphere.obj" scene (not a shipped scene file): 1298 triangles, BVH
+SPHERE = CORNELL + [ObjectSpec(os.path.join(ASSETS, "shapes", "sphere.obj"), "*Kd 0.2 0.6 0.3*", (0.3, -1.2, 4.2),
+                               (0.0, 0.4, 0.0), (1.2, 1.2, 1.2))]
 # casts/sample counted by the CPU oracle over the full C2
 # frame (tools/count_casts.py -> profiles/casts_per_sample.json)
 CASTS_PER_SAMPLE = 5.694442272186279
@@ -176,6 +183,38 @@ def main():
     e1.record(stream)
     barrier()
     bwd_ms = max_over_ranks(e0.elapsed_time(e1))
+    # ------------------------------------------- secondary workloads (info)
+    extra = {}
+    for key, objs, kind in (("c3_grad", SCENE0, "adj"), ("bvh_fwd", SPHERE, "fwd")):
+        sc = Scene(objs)
+        g2 = torch.zeros((sc.nT, 3), device=dev, dtype=torch.float64)
+
+        def run(step):
+            p = params(step)
+            if kind == "adj":
+                g2.zero_()
+                N.check(L.ipt_adjoint_dev(sc.handle, C.byref(p), None, adj.data_ptr(), g2.data_ptr(), st))
+                if world > 1:
+                    dist.all_reduce(g2)
+            else:
+                N.check(L.ipt_render_samples_sm_dev(sc.handle, C.byref(p), None, samples.data_ptr(), st))
+
+        k = max(1, min(args.steps, 5))
+        run(10**6)
+        barrier()
+        e0.record(stream)
+        for i in range(k):
+            run(i)
+        e1.record(stream)
+        barrier()
+        ms = max_over_ranks(e0.elapsed_time(e1)) / k
+        extra[key] = {"value": round(world * W * H * SPP / ms / 1e3, 2),
+                      "unit": "grad-Msamples/s" if kind == "adj" else "Msamples/s", "ms_per_step": round(ms, 4),
+                      "triangles": sc.nT, "accel": sc.bvh_info()["accel"],
+                      "workload": ("C3: scenes/0.txt (Cornell + cube), 512x512, 64 spp, 4 bounces, adjoint dL/dKd "
+                                   "+ all-reduce" if kind == "adj" else
+                                   "Cornell + sphere.obj (north_star scene), 512x512, 64 spp, 4 bounces, forward")}
+        sc.close()
 
     samples_per_frame = W * H * SPP
     value = world * args.steps * samples_per_frame / (fwd_ms / 1e3) / 1e6
@@ -217,7 +256,7 @@ def main():
             "grad_value": round(grad_value, 2), "grad_unit": "grad-Msamples/s",
             "grad_ms_per_step": round(bwd_ms / args.steps, 4),
             "wall_s_fwd_region": round(wall_fwd, 4),
-            "roofline": roofline, "hbm": hbm, "cpu_baseline": cpu,
+            "roofline": roofline, "hbm": hbm, "cpu_baseline": cpu, "secondary": extra,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -586,32 +586,13 @@ __device__ __forceinline__ void bvh_big_pass(const BvhView &B, V3 p, V3 d, float
   }
 }
 
-// Closest hit through the BVH.  target < 0: ordinary cast.  target >= 0
-// (next-event shadow ray towards emitter triangle `target`): the caller only
-// needs to know whether the closest hit IS `target` (and its t), so the
-// target is tested first, its (t, index) seeds the search -- pruning every box
-// beyond it -- and the first triangle found ahead of it ends the traversal
-// (result != target, exactly as the full search would conclude).  Returns the
-// hit's original triangle index or -1.
-template <bool SHADOW>
-__device__ __forceinline__ int closest_hit_bvh(const BvhView &B, V3 p, V3 d, float &best_t, int target = -1) {
-  float bt = __builtin_inff();
-  int bi = -1;
-  if (SHADOW) {
-    hit_test(B.isect[target], target, p, d, bt, bi);
-    if (bi < 0) {
-      best_t = bt;
-      return -1;  // the target itself is missed: not the closest hit either
-    }
-  }
-  if (B.nbig > 0) {
-    bvh_big_pass(B, p, d, bt, bi);
-    if (SHADOW && bi != target) {  // occluded by a large triangle: decided
-      best_t = bt;
-      return bi;
-    }
-  }
-  // slab parameters t = fma(box, 1/d, -p/d); |d| < 2^-60: slab ignored (NaN)
+// Slab form of a ray: t = fma(box, 1/d, -p/d) per axis; |d| < 2^-60 makes
+// that axis's parameters NaN, which min/max ignore (the slab is dropped:
+// conservative).  bvh.cpp states why the rounding of this form is covered.
+struct SlabRay {
+  f2 ix, iy, iz, ox, oy, oz;
+};
+__device__ __forceinline__ SlabRay slab_ray(V3 p, V3 d) {
   const float qnan = __builtin_nanf("");
   const float ix = fabsf(d.x) < 0x1p-60f ? 0.f : __builtin_amdgcn_rcpf(d.x);
   const float iy = fabsf(d.y) < 0x1p-60f ? 0.f : __builtin_amdgcn_rcpf(d.y);
@@ -619,7 +600,60 @@ __device__ __forceinline__ int closest_hit_bvh(const BvhView &B, V3 p, V3 d, flo
   const float ox = fabsf(d.x) < 0x1p-60f ? qnan : -(p.x * ix);
   const float oy = fabsf(d.y) < 0x1p-60f ? qnan : -(p.y * iy);
   const float oz = fabsf(d.z) < 0x1p-60f ? qnan : -(p.z * iz);
-  const f2 ix2 = bc2(ix), iy2 = bc2(iy), iz2 = bc2(iz), ox2 = bc2(ox), oy2 = bc2(oy), oz2 = bc2(oz);
+  return SlabRay{bc2(ix), bc2(iy), bc2(iz), bc2(ox), bc2(oy), bc2(oz)};
+}
+// Both children's boxes of an inner node against [0, bt]: h0/h1 = hit,
+// en0/en1 = entry parameters, c0/c1 = child links.
+__device__ __forceinline__ void bvh_node_test(const BvhView &B, int node, const SlabRay &r, float bt, bool &h0,
+                                              bool &h1, float &en0, float &en1, int &c0, int &c1) {
+  float4 q0, q1, q2, q3;
+  bvh_load_node(B, node, q0, q1, q2, q3);
+  const f2 tx0 = fma2(f2{q0.x, q1.z}, r.ix, r.ox), tx1 = fma2(f2{q0.y, q1.w}, r.ix, r.ox);
+  const f2 ty0 = fma2(f2{q0.z, q2.x}, r.iy, r.oy), ty1 = fma2(f2{q0.w, q2.y}, r.iy, r.oy);
+  const f2 tz0 = fma2(f2{q1.x, q2.z}, r.iz, r.oz), tz1 = fma2(f2{q1.y, q2.w}, r.iz, r.oz);
+  en0 = fmaxf(fmaxf(fminf(tx0.x, tx1.x), fminf(ty0.x, ty1.x)), fmaxf(fminf(tz0.x, tz1.x), 0.f));
+  const float ex0 = fminf(fminf(fmaxf(tx0.x, tx1.x), fmaxf(ty0.x, ty1.x)), fminf(fmaxf(tz0.x, tz1.x), bt));
+  en1 = fmaxf(fmaxf(fminf(tx0.y, tx1.y), fminf(ty0.y, ty1.y)), fmaxf(fminf(tz0.y, tz1.y), 0.f));
+  const float ex1 = fminf(fminf(fmaxf(tx0.y, tx1.y), fmaxf(ty0.y, ty1.y)), fminf(fmaxf(tz0.y, tz1.y), bt));
+  h0 = en0 <= ex0;
+  h1 = en1 <= ex1;
+  c0 = __float_as_int(q3.x);
+  c1 = __float_as_int(q3.y);
+}
+
+// The part of a cast done before the traversal: the shadow target's own
+// test (target >= 0) and the large-triangle pre-pass.  Returns false when
+// the cast is already decided (shadow target missed or occluded).
+template <bool SHADOW>
+__device__ __forceinline__ bool bvh_prepass(const BvhView &B, V3 p, V3 d, float &bt, int &bi, int target) {
+  bt = __builtin_inff();
+  bi = -1;
+  if (SHADOW) {
+    hit_test(B.isect[target], target, p, d, bt, bi);
+    if (bi < 0) return false;  // the target itself is missed: not the closest hit either
+  }
+  if (B.nbig > 0) {
+    bvh_big_pass(B, p, d, bt, bi);
+    if (SHADOW && bi != target) return false;  // occluded by a large triangle: decided
+  }
+  return true;
+}
+
+// Does the ray reach either child of the root within [0, bt]?  (If not, the
+// traversal cannot change (bt, bi).)
+__device__ __forceinline__ bool bvh_root_test(const BvhView &B, V3 p, V3 d, float bt) {
+  bool h0, h1;
+  float en0, en1;
+  int c0, c1;
+  bvh_node_test(B, 0, slab_ray(p, d), bt, h0, h1, en0, en1, c0, c1);
+  return h0 || h1;
+}
+
+// The traversal proper from the root, continuing the lexicographic minimum
+// (bt, bi).  SHADOW: stops as soon as bi is no longer `target` (occluded).
+template <bool SHADOW, int STRIDE = kStackStride>
+__device__ __forceinline__ void bvh_traverse(const BvhView &B, V3 p, V3 d, float &bt, int &bi, int target) {
+  const SlabRay r = slab_ray(p, d);
   uint32_t *stk = B.stack;
   int sp = 0;
   int node = 0;
@@ -631,26 +665,19 @@ __device__ __forceinline__ int closest_hit_bvh(const BvhView &B, V3 p, V3 d, flo
 #ifdef IPT_BVH_STATS
       ++st_nodes;
 #endif
-      float4 q0, q1, q2, q3;
-      bvh_load_node(B, node, q0, q1, q2, q3);
-      const f2 tx0 = fma2(f2{q0.x, q1.z}, ix2, ox2), tx1 = fma2(f2{q0.y, q1.w}, ix2, ox2);
-      const f2 ty0 = fma2(f2{q0.z, q2.x}, iy2, oy2), ty1 = fma2(f2{q0.w, q2.y}, iy2, oy2);
-      const f2 tz0 = fma2(f2{q1.x, q2.z}, iz2, oz2), tz1 = fma2(f2{q1.y, q2.w}, iz2, oz2);
-      const float en0 = fmaxf(fmaxf(fminf(tx0.x, tx1.x), fminf(ty0.x, ty1.x)), fmaxf(fminf(tz0.x, tz1.x), 0.f));
-      const float ex0 = fminf(fminf(fmaxf(tx0.x, tx1.x), fmaxf(ty0.x, ty1.x)), fminf(fmaxf(tz0.x, tz1.x), bt));
-      const float en1 = fmaxf(fmaxf(fminf(tx0.y, tx1.y), fminf(ty0.y, ty1.y)), fmaxf(fminf(tz0.y, tz1.y), 0.f));
-      const float ex1 = fminf(fminf(fmaxf(tx0.y, tx1.y), fmaxf(ty0.y, ty1.y)), fminf(fmaxf(tz0.y, tz1.y), bt));
-      const bool h0 = en0 <= ex0, h1 = en1 <= ex1;
-      const int c0 = __float_as_int(q3.x), c1 = __float_as_int(q3.y);
+      bool h0, h1;
+      float en0, en1;
+      int c0, c1;
+      bvh_node_test(B, node, r, bt, h0, h1, en0, en1, c0, c1);
       if (h0 && h1) {
         const bool first0 = en0 <= en1;
-        stk[sp * kStackStride] = (uint32_t)(first0 ? c1 : c0);
+        stk[sp * STRIDE] = (uint32_t)(first0 ? c1 : c0);
         ++sp;
         node = first0 ? c0 : c1;
       } else if (h0 || h1) {
         node = h0 ? c0 : c1;
       } else {
-        node = sp > 0 ? (int)stk[--sp * kStackStride] : kBvhDone;
+        node = sp > 0 ? (int)stk[--sp * STRIDE] : kBvhDone;
       }
     }
     if (node != kBvhDone) {  // leaf
@@ -660,7 +687,7 @@ __device__ __forceinline__ int closest_hit_bvh(const BvhView &B, V3 p, V3 d, flo
 #ifdef IPT_BVH_STATS
       st_pairs += np;
 #endif
-      node = sp > 0 ? (int)stk[--sp * kStackStride] : kBvhDone;
+      node = sp > 0 ? (int)stk[--sp * STRIDE] : kBvhDone;
       if (SHADOW && bi != target) node = kBvhDone;  // occluded: decided
     }
   }
@@ -670,6 +697,24 @@ __device__ __forceinline__ int closest_hit_bvh(const BvhView &B, V3 p, V3 d, flo
   atomicAdd(&g_bvh_stats[2], (unsigned long long)st_pairs);
   if (SHADOW && bi != target) atomicAdd(&g_bvh_stats[3], 1ull);
 #endif
+}
+
+// Closest hit through the BVH, one lane per ray.  target < 0: ordinary cast.
+// target >= 0 (next-event shadow ray towards emitter triangle `target`): the
+// caller only needs to know whether the closest hit IS `target` (and its t),
+// so the target is tested first, its (t, index) seeds the search -- pruning
+// every box beyond it -- and the first triangle found ahead of it ends the
+// traversal (result != target, exactly as the full search would conclude).
+// Returns the hit's original triangle index or -1.
+template <bool SHADOW>
+__device__ __forceinline__ int closest_hit_bvh(const BvhView &B, V3 p, V3 d, float &best_t, int target = -1) {
+  float bt;
+  int bi;
+  if (bvh_prepass<SHADOW>(B, p, d, bt, bi, target)) {
+#ifndef IPT_ABL_NOTRAV  // timing-only ablation build: pre-pass only, no traversal
+    bvh_traverse<SHADOW>(B, p, d, bt, bi, target);
+#endif
+  }
   best_t = bt;
   return bi;
 }

@@ -150,7 +150,23 @@ constexpr int min_blocks() {
   return BVH ? IPT_MIN_BLOCKS_BVH
              : (MODE == 0 ? IPT_MIN_BLOCKS_FWD : (MODE == 1 ? IPT_MIN_BLOCKS_ADJ : IPT_MIN_BLOCKS_GRAPH));
 }
-#define IPT_TRACE_BOUNDS __attribute__((amdgpu_flat_work_group_size(1, kBlock), amdgpu_waves_per_eu(min_blocks<MODE, BVH>() ? min_blocks<MODE, BVH>() : 1)))
+// IPT_BVH_SERVER=1: BVH instances run 4 path waves + 1 traversal-server
+// wave per workgroup (ray compaction through an LDS queue, see trace_kernel).
+// Exact like the default, but measured SLOWER on the sphere scene (C2 size:
+// 21.0 vs 13.3 ms forward, profiles/r01_bvh_server.log): the traversal is
+// latency-bound (about 13 dependent node/leaf steps for the rays that reach
+// the tree), and funnelling every block's rays through one wave serialises
+// those chains behind two extra barriers per cast, while the VALU slots it
+// frees were not the bottleneck.  Off by default.
+#ifndef IPT_BVH_SERVER
+#define IPT_BVH_SERVER 0
+#endif
+constexpr int kBlockSrv = kBlock + 64;
+template <bool BVH>
+constexpr int block_threads() {
+  return (BVH && IPT_BVH_SERVER) ? kBlockSrv : kBlock;
+}
+#define IPT_TRACE_BOUNDS __attribute__((amdgpu_flat_work_group_size(1, block_threads<BVH>()), amdgpu_waves_per_eu(min_blocks<MODE, BVH>() ? min_blocks<MODE, BVH>() : 1)))
 // Profiling-only build (make variant DEFS=-DIPT_PHASE_TIMING): each wave
 // accumulates s_memtime cycles per phase of the loop; read with
 // ipt_debug_phase_cycles (tools/phase_timing.py).
@@ -194,6 +210,55 @@ __device__ __forceinline__ int cast(const TriIsect *__restrict__ isect, const Tr
   return cast_bf(isect, pairs, e3, nT, p, d, t);
 }
 
+// ---- BVH ray compaction (the north_star's "wavefront ballot/prefix for ray
+// compaction").  In a BVH scene each path wave casts its rays through the
+// large-triangle pre-pass and the root test itself; the few rays that do
+// reach the tree (typically ~10% of lanes, spread over every wave) are
+// appended, by ballot + mbcnt prefix, to the workgroup's LDS queue, and ONE
+// server wave traverses them densely -- 64 rays per pass instead of four
+// waves each running the traversal loop for a handful of lanes.  Queue:
+// [field][slot], field = p.xyz, d.xyz, bt, bi; slot = 64 * path wave + rank.
+constexpr int kQFields = 8;
+constexpr int kQSlots = kBlock;
+__device__ __forceinline__ void srv_put(float *q, int slot, V3 p, V3 d, float bt, int bi) {
+  q[0 * kQSlots + slot] = p.x;
+  q[1 * kQSlots + slot] = p.y;
+  q[2 * kQSlots + slot] = p.z;
+  q[3 * kQSlots + slot] = d.x;
+  q[4 * kQSlots + slot] = d.y;
+  q[5 * kQSlots + slot] = d.z;
+  q[6 * kQSlots + slot] = bt;
+  q[7 * kQSlots + slot] = __int_as_float(bi);
+}
+__device__ __forceinline__ int lane_rank(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+// Server wave: traverse every queued ray (counts[w] entries of path wave w),
+// 64 per pass, and write (bt, bi) back.  A shadow entry's initial bi is its
+// target (the pre-pass found it unoccluded so far).
+template <bool SHADOW>
+__device__ __forceinline__ void srv_serve(const BvhView &B, float *q, const int *counts, int lane) {
+  const int c0 = counts[0], c1 = counts[1], c2 = counts[2], c3 = counts[3];
+  const int n = c0 + c1 + c2 + c3;
+  for (int base = 0; base < n; base += 64) {
+    const int g = base + lane;
+    if (g < n) {
+      int slot;
+      if (g < c0) slot = g;
+      else if (g < c0 + c1) slot = 64 + (g - c0);
+      else if (g < c0 + c1 + c2) slot = 128 + (g - c0 - c1);
+      else slot = 192 + (g - c0 - c1 - c2);
+      const V3 p = mk(q[0 * kQSlots + slot], q[1 * kQSlots + slot], q[2 * kQSlots + slot]);
+      const V3 d = mk(q[3 * kQSlots + slot], q[4 * kQSlots + slot], q[5 * kQSlots + slot]);
+      float bt = q[6 * kQSlots + slot];
+      int bi = __float_as_int(q[7 * kQSlots + slot]);
+      bvh_traverse<SHADOW, 64>(B, p, d, bt, bi, bi);
+      q[6 * kQSlots + slot] = bt;
+      q[7 * kQSlots + slot] = __int_as_float(bi);
+    }
+  }
+}
+
 // LDS carve-out of the BVH instances: node copy (16-B aligned) + stack.
 __host__ __device__ inline size_t bvh_lds_offset(size_t base) { return (base + 15) & ~(size_t)15; }
 
@@ -207,6 +272,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     double *__restrict__ edges) {
   extern __shared__ double lds[];
   const int tid = threadIdx.x;
+  constexpr bool SERVE = BVH && IPT_BVH_SERVER;  // + a traversal-server wave
+  constexpr int nthr = block_threads<BVH>();
   const int nT = a.nT, nE = a.nE;
   const int vmax = a.max_bounces + 1;  // ADJ record capacity per lane
   // LDS: [fp64 accumulators][kd table][kd/pi table][ADJ vertex records]
@@ -225,7 +292,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   const float *kd_t = kd;   // kd[3*tri]
   const float *kdpi_t = tab + 3 * nT;
   if (a.kd_tables) {
-    for (int i = tid; i < 3 * nT; i += kBlock) {
+    for (int i = tid; i < 3 * nT; i += nthr) {
       const float v = kd[i];
       tab[i] = v;
       tab[3 * nT + i] = v / kPiF;
@@ -238,7 +305,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   float *lds_e3 = tab + (a.kd_tables ? 6 * nT : 0);
   const int nP = (nT + 1) >> 1;
   if (a.small_pairs) {
-    for (int i = tid; i < 6 * nP; i += kBlock) {
+    for (int i = tid; i < 6 * nP; i += nthr) {
       const int j = i / 6, kf = (i % 6) >> 1, h = i & 1;
       lds_e3[i] = pairs[j].f[9 + 4 * kf][h];
     }
@@ -255,6 +322,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   bv.big_idx = nullptr;
   bv.big_e3 = nullptr;
   bv.nbig = 0;
+  float *srvq = nullptr;  // SERVE: ray queue [kQFields][kQSlots]
+  int *srvc = nullptr;    // SERVE: per path wave queued count [4], live flag [4]
   if (BVH) {
     const size_t rec_words = (MODE == MODE_ADJ) ? (size_t)vmax * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock : 0;
     char *base = reinterpret_cast<char *>(lds);
@@ -262,11 +331,11 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     float4 *ln = reinterpret_cast<float4 *>(base + off);
     if (a.bvh_lds_nodes > 0) {
       const float4 *g = reinterpret_cast<const float4 *>(bnodes);
-      for (int i = tid; i < 4 * a.bvh_lds_nodes; i += kBlock) ln[i] = g[i];
+      for (int i = tid; i < 4 * a.bvh_lds_nodes; i += nthr) ln[i] = g[i];
       bv.lnodes = ln;
     }
     float *be3 = reinterpret_cast<float *>(ln + 4 * a.bvh_lds_nodes);
-    for (int i = tid; i < 6 * a.bvh_nbig; i += kBlock) {
+    for (int i = tid; i < 6 * a.bvh_nbig; i += nthr) {
       const int j = i / 6, kf = (i % 6) >> 1, h = i & 1;
       be3[i] = a.bvh_big[j].f[9 + 4 * kf][h];
     }
@@ -274,12 +343,20 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     bv.big_idx = a.bvh_big_idx;
     bv.big_e3 = reinterpret_cast<const f2 *>(be3);
     bv.nbig = a.bvh_nbig;
-    bv.stack = reinterpret_cast<uint32_t *>(be3 + 6 * a.bvh_nbig) + tid;
+    float *after = be3 + 6 * a.bvh_nbig;
+    if (SERVE) {
+      srvq = after;
+      srvc = reinterpret_cast<int *>(srvq + kQFields * kQSlots);
+      bv.stack = reinterpret_cast<uint32_t *>(srvc + 8) + (tid >= kBlock ? tid - kBlock : 0);  // stride 64
+    } else {
+      bv.stack = reinterpret_cast<uint32_t *>(after) + tid;
+    }
   }
-  for (int i = tid; i < n_acc; i += kBlock) lds_acc[i] = 0.0;
+  for (int i = tid; i < n_acc; i += nthr) lds_acc[i] = 0.0;
   __syncthreads();
   double *acc = (MODE == MODE_GRAPH && !a.lds_edges) ? edges : lds_acc;
 
+  if (!SERVE || tid < kBlock) {  // path waves
   // wave-uniform sample range (static partition, regenerated per lane)
   const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * kBlock + tid) >> 6);
   const uint32_t nwaves = (gridDim.x * kBlock) >> 6;
@@ -369,7 +446,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       next += (uint64_t)__popcll(need);
     }
     PHASE(0)
-    if (__ballot(active) == 0) break;
+    if (!SERVE && __ballot(active) == 0) break;
 #ifdef IPT_PHASE_TIMING
     tacc[6] += 1;
     tacc[7] += __popcll(__ballot(active));
@@ -378,7 +455,31 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     // ================= phase 1: path ray (radiance, path_trace.cu:111-144)
     float t = 0.f;
     int hit = -1;
-    if (active) hit = cast<BVH>(isect, pairs, e3, nT, bv, p, d, t, -1);
+    if (SERVE) {  // pre-pass + root test here; the tree part via the server wave
+      const int wl = tid >> 6;
+      bool qn = false;
+      if (active) {
+        bvh_prepass<false>(bv, p, d, t, hit, -1);
+        qn = bvh_root_test(bv, p, d, t);
+      }
+      const uint64_t qm = __ballot(qn);
+      const int slot = 64 * wl + lane_rank(qm);
+      if (qn) srv_put(srvq, slot, p, d, t, hit);
+      const bool live = __ballot(active) != 0;
+      if ((tid & 63) == 0) {
+        srvc[wl] = (int)__popcll(qm);
+        srvc[4 + wl] = live ? 1 : 0;
+      }
+      __syncthreads();  // B: queue + liveness published
+      if (!(srvc[4] | srvc[5] | srvc[6] | srvc[7])) break;  // the whole workgroup is done
+      __syncthreads();  // C: the server has traversed the queue
+      if (qn) {
+        t = srvq[6 * kQSlots + slot];
+        hit = __float_as_int(srvq[7 * kQSlots + slot]);
+      }
+    } else if (active) {
+      hit = cast<BVH>(isect, pairs, e3, nT, bv, p, d, t, -1);
+    }
     PHASE(1)
     const bool vertex = active && hit >= 0;
     bool finished = false, escaped = false;
@@ -480,11 +581,26 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     V3 lo = mk(0.f, 0.f, 0.f);
     float emit_s = 0.f;  // ADJ record: lo = Ke[emit_et] * emit_s
     int emit_et = 0;
+    float ts = 0.f;
+    int hs = -1;
+    const int et = shadow ? emit_tri[emitter] : -1;
+    if (SERVE) {  // same split as the path ray, with the shadow early-out
+      const int wl = tid >> 6;
+      bool qn = false;
+      if (shadow && bvh_prepass<true>(bv, p, sd, ts, hs, et)) qn = bvh_root_test(bv, p, sd, ts);
+      const uint64_t qm = __ballot(qn);
+      const int slot = 64 * wl + lane_rank(qm);
+      if (qn) srv_put(srvq, slot, p, sd, ts, hs);
+      if ((tid & 63) == 0) srvc[wl] = (int)__popcll(qm);
+      __syncthreads();  // D: shadow queue published
+      __syncthreads();  // E: the server has traversed it
+      if (qn) {
+        ts = srvq[6 * kQSlots + slot];
+        hs = __float_as_int(srvq[7 * kQSlots + slot]);
+      }
+    }
     if (__ballot(shadow)) {
-      float ts = 0.f;
-      int hs = -1;
-      const int et = shadow ? emit_tri[emitter] : -1;
-      if (shadow) hs = cast<BVH>(isect, pairs, e3, nT, bv, p, sd, ts, et);
+      if (!SERVE && shadow) hs = cast<BVH>(isect, pairs, e3, nT, bv, p, sd, ts, et);
       PHASE(3)
       if (shadow && hs == et) {  // must hit the sampled emitter itself
         const V3 ne = shading_normal(geom[et], along(p, sd, ts));
@@ -674,11 +790,24 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     for (int i = 0; i < 8; ++i) atomicAdd(&g_phase_cycles[i], (unsigned long long)tacc[i]);
 #endif
 
+  } else {  // traversal-server wave: mirrors the path waves' barriers B..E
+    const int lane = tid - kBlock;
+    for (;;) {
+      __syncthreads();  // B
+      if (!(srvc[4] | srvc[5] | srvc[6] | srvc[7])) break;
+      srv_serve<false>(bv, srvq, srvc, lane);
+      __syncthreads();  // C
+      __syncthreads();  // D
+      srv_serve<true>(bv, srvq, srvc, lane);
+      __syncthreads();  // E
+    }
+  }
+
   if (MODE != MODE_FWD) {
     __syncthreads();
     if (n_acc > 0) {
       double *dstp = (MODE == MODE_ADJ) ? grad : edges;
-      for (int i = tid; i < n_acc; i += kBlock) {
+      for (int i = tid; i < n_acc; i += nthr) {
         const double v = lds_acc[i];
         const int j = (MODE == MODE_ADJ && a.slot_tri) ? a.slot_tri[i / 3] * 3 + i % 3 : i;
         if (v != 0.0) atomicAdd(dstp + j, v);
@@ -900,7 +1029,8 @@ static int resident_grid(GpuScene *s, size_t lds_bytes, int *grid) {
   const int slot = MODE * 4 + (SPEC ? 2 : 0) + (BVH ? 1 : 0);
   if (s->grid[slot] == 0 || s->grid_lds[slot] != lds_bytes) {
     int per_cu = 0, cus = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<MODE, SPEC, BVH>, kBlock, lds_bytes));
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<MODE, SPEC, BVH>, block_threads<BVH>(),
+                                                         lds_bytes));
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device));
     if (per_cu <= 0) {
       gpu_set_error("trace kernel cannot be resident (LDS request too large?)");
@@ -960,15 +1090,20 @@ static bool use_bvh(const GpuScene *s) {
 }
 
 // BVH LDS carve-out on top of `base` bytes; fills the args' BVH fields.
-static size_t bvh_lds(const GpuScene *s, TraceArgs &a, size_t base) {
+// server: the megakernel's layout (ray queue + a 64-lane stack); else one
+// stack per thread of a 256-thread block (the closest-hit probe).
+static size_t bvh_lds(const GpuScene *s, TraceArgs &a, size_t base, bool server) {
   const size_t nn = s->host.bvh_nodes.size();
   a.bvh_lds_nodes = nn * sizeof(BvhNode) <= (size_t)kBvhLdsNodeBytes ? (int)nn : 0;
   a.bvh_stack = std::max(1, s->host.bvh_depth);
   a.bvh_nbig = (int)s->host.bvh_big_pairs.size();
   a.bvh_big = s->big_pairs;
   a.bvh_big_idx = s->big_idx;
-  return bvh_lds_offset(base) + (size_t)a.bvh_lds_nodes * sizeof(BvhNode) + (size_t)a.bvh_nbig * 6 * sizeof(float) +
-         (size_t)a.bvh_stack * kBlock * sizeof(uint32_t);
+  const size_t head = bvh_lds_offset(base) + (size_t)a.bvh_lds_nodes * sizeof(BvhNode) +
+                      (size_t)a.bvh_nbig * 6 * sizeof(float);
+  if (server)
+    return head + (size_t)kQFields * kQSlots * sizeof(float) + 8 * sizeof(int) + (size_t)a.bvh_stack * 64 * sizeof(uint32_t);
+  return head + (size_t)a.bvh_stack * kBlock * sizeof(uint32_t);
 }
 
 static size_t table_bytes(const TraceArgs &a) {
@@ -986,7 +1121,7 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
   }
   if (resident_grid<MODE, SPEC, BVH>(s, lds, &grid)) return -1;
   if (a.n_samples == 0) return 0;
-  hipLaunchKernelGGL((trace_kernel<MODE, SPEC, BVH>), dim3(grid), dim3(kBlock), lds, st, s->isect, s->pairs, s->geom,
+  hipLaunchKernelGGL((trace_kernel<MODE, SPEC, BVH>), dim3(grid), dim3(block_threads<BVH>()), lds, st, s->isect, s->pairs, s->geom,
                      s->mat, s->bnodes, s->bpairs, kd_dev ? kd_dev : s->kd, s->emit_tri, s->emit_cdf, s->emit_pmf, a,
                      out, adj, grad, target, edges);
   HIP_TRY(hipGetLastError());
@@ -1001,7 +1136,7 @@ template <int MODE>
 static int launch(GpuScene *s, TraceArgs a, size_t lds, const float *kd_dev, float *out, const float *adj,
                   double *grad, const uint8_t *target, double *edges, hipStream_t st) {
   if (use_bvh(s)) {
-    lds = bvh_lds(s, a, lds);
+    lds = bvh_lds(s, a, lds, IPT_BVH_SERVER != 0);
     if (s->has_ks) return launch_inst<MODE, true, true>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
     return launch_inst<MODE, false, true>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
   }
@@ -1310,7 +1445,7 @@ int gpu_closest_hit(GpuScene *s, int64_t n, const float *org_dev, const float *d
   const size_t base = small ? (size_t)6 * ((s->host.nT + 1) / 2) * sizeof(float) : 0;
   const int blocks = (int)((n + kBlock - 1) / kBlock);
   if (use_bvh(s)) {
-    const size_t lds = bvh_lds(s, a, base);
+    const size_t lds = bvh_lds(s, a, base, false);
     hipLaunchKernelGGL(closest_hit_kernel<true>, dim3(blocks), dim3(kBlock), lds, (hipStream_t)stream, s->isect,
                        s->pairs, s->bnodes, s->bpairs, s->host.nT, small, a.bvh_lds_nodes, a.bvh_big, a.bvh_big_idx,
                        a.bvh_nbig, n, org_dev, dir_dev, targets_dev, t_dev, idx_dev);
