@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the C3/C4/BVH-scene lines (profiling runs: keeps the C2 kernel's statistics pure)")
     return ap.parse_args()
 
 
@@ -185,7 +187,7 @@ def main():
     bwd_ms = max_over_ranks(e0.elapsed_time(e1))
     # ------------------------------------------- secondary workloads (info)
     extra = {}
-    for key, objs, kind in (("c3_grad", SCENE0, "adj"), ("bvh_fwd", SPHERE, "fwd")):
+    for key, objs, kind in (() if args.no_secondary else (("c3_grad", SCENE0, "adj"), ("bvh_fwd", SPHERE, "fwd"))):
         sc = Scene(objs)
         g2 = torch.zeros((sc.nT, 3), device=dev, dtype=torch.float64)
 
@@ -215,6 +217,44 @@ def main():
                                    "+ all-reduce" if kind == "adj" else
                                    "Cornell + sphere.obj (north_star scene), 512x512, 64 spp, 4 bounces, forward")}
         sc.close()
+    # C4 (BASELINE.json configs[3]): scenes/0.txt, 1024x1024, 256 spp, 8 bounces,
+    # rank k traces row band k of 8 (the 8-GPU sharding); forward + adjoint
+    # with the one gradient all-reduce.  At N < 8 only bands 0..N-1 run.
+    if world <= 8 and not args.no_secondary:
+        from inverse_path_tracer_amd.distributed import shard_rows
+        W4, S4, B4 = 1024, 256, 8
+        b4, e4 = shard_rows(W4, 8, rank)
+        sc = Scene(SCENE0)
+        g4 = torch.zeros((sc.nT, 3), device=dev, dtype=torch.float64)
+        adj4 = torch.full((W4, W4, 3), 1.0 / (3 * W4 * W4), device=dev, dtype=torch.float32)
+        smp4 = torch.empty(((e4 - b4) * W4 * S4, 3), device=dev, dtype=torch.float32)
+        p4 = N.make_params(W4, W4, S4, B4, args.seed, b4, e4)
+        res4 = {}
+        for kind in ("fwd", "adj"):
+            def run4():
+                if kind == "fwd":
+                    N.check(L.ipt_render_samples_sm_dev(sc.handle, C.byref(p4), None, smp4.data_ptr(), st))
+                else:
+                    g4.zero_()
+                    N.check(L.ipt_adjoint_dev(sc.handle, C.byref(p4), None, adj4.data_ptr(), g4.data_ptr(), st))
+                    if world > 1:
+                        dist.all_reduce(g4)
+            run4()
+            barrier()
+            e0.record(stream)
+            for _ in range(2):
+                run4()
+            e1.record(stream)
+            barrier()
+            res4[kind] = max_over_ranks(e0.elapsed_time(e1)) / 2
+        n4 = world * (e4 - b4) * W4 * S4
+        extra["c4"] = {"value": round(n4 / res4["fwd"] / 1e3, 2), "unit": "Msamples/s",
+                       "grad_value": round(n4 / res4["adj"] / 1e3, 2), "grad_unit": "grad-Msamples/s",
+                       "fwd_ms": round(res4["fwd"], 3), "adj_ms": round(res4["adj"], 3), "bands": "%d of 8" % world,
+                       "workload": "C4: scenes/0.txt, 1024x1024, 256 spp, 8 bounces; rank k = row band k of 8 "
+                                   "(forward, adjoint + all-reduce)"}
+        sc.close()
+        del smp4
 
     samples_per_frame = W * H * SPP
     value = world * args.steps * samples_per_frame / (fwd_ms / 1e3) / 1e6
