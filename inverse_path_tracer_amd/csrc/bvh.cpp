@@ -288,6 +288,105 @@ int acceptance_box(const TriIsect &T, const TriGeom &G, double r_all, float lo[3
   return 0;
 }
 
+// Collapse the binary tree into 8-wide nodes: starting from a binary node's
+// two children, repeatedly open the inner child with the largest box until
+// the node has 8 children or only leaves remain.  Leaves keep their binary
+// triangle sets (<= 16 triangles), re-laid as single TriIsect records.
+static bool build_wide(HostScene *S) {
+  struct Child {
+    float lo[3], hi[3];
+    int code;  // binary child code
+  };
+  auto child_of = [&](int n, int c) {
+    const BvhNode &N = S->bvh_nodes[(size_t)n];
+    Child ch;
+    const float *q = &N.q[0][0];
+    for (int a = 0; a < 3; ++a) {
+      ch.lo[a] = q[6 * c + 2 * a];
+      ch.hi[a] = q[6 * c + 2 * a + 1];
+    }
+    int kid[2];
+    std::memcpy(kid, &N.q[3][0], sizeof kid);
+    ch.code = kid[c];
+    return ch;
+  };
+  auto area = [](const Child &c) {
+    const double dx = (double)c.hi[0] - c.lo[0], dy = (double)c.hi[1] - c.lo[1], dz = (double)c.hi[2] - c.lo[2];
+    return dx * dy + dy * dz + dz * dx;
+  };
+  S->bvh_wide.clear();
+  S->bvh_wtris.clear();
+  S->bvh_wdepth = 0;
+  // root box
+  {
+    const Child c0 = child_of(0, 0), c1 = child_of(0, 1);
+    for (int a = 0; a < 3; ++a) {
+      S->bvh_root_box[a] = std::min(c0.lo[a], c1.lo[a]);
+      S->bvh_root_box[3 + a] = std::max(c0.hi[a], c1.hi[a]);
+    }
+  }
+  // breadth-first over wide nodes, each given by its binary node
+  std::vector<std::pair<int, int>> queue;  // (binary node, wide depth)
+  queue.push_back({0, 1});
+  for (size_t h = 0; h < queue.size(); ++h) {
+    const int bn = queue[h].first, depth = queue[h].second;
+    S->bvh_wdepth = std::max(S->bvh_wdepth, depth);
+    std::vector<Child> kids = {child_of(bn, 0), child_of(bn, 1)};
+    while (kids.size() < 8) {
+      int best = -1;
+      for (size_t k = 0; k < kids.size(); ++k)
+        if (kids[k].code >= 0 && (best < 0 || area(kids[k]) > area(kids[(size_t)best]))) best = (int)k;
+      if (best < 0) break;
+      const int n = kids[(size_t)best].code;
+      kids[(size_t)best] = child_of(n, 0);
+      kids.push_back(child_of(n, 1));
+    }
+    WideNode W;
+    std::memset(&W, 0, sizeof W);
+    for (int k = 0; k < 8; ++k) {
+      float *sl = W.s[k];
+      int32_t ref = kWideEmpty;
+      if (k < (int)kids.size()) {
+        const Child &c = kids[(size_t)k];
+        for (int a = 0; a < 3; ++a) {
+          sl[a] = c.lo[a];
+          sl[3 + a] = c.hi[a];
+        }
+        if (c.code >= 0) {
+          ref = (int32_t)queue.size();  // wide node h is queue[h]: a child's index is its queue position
+          queue.push_back({c.code, depth + 1});
+        } else {
+          const int code = ~c.code;
+          const int first = code >> kBvhLeafPairBits, np = (code & ((1 << kBvhLeafPairBits) - 1)) + 1;
+          const int tfirst = (int)S->bvh_wtris.size();
+          for (int j = first; j < first + np; ++j)
+            for (int hh = 0; hh < 2; ++hh) {
+              const int t = S->bvh_pairs[(size_t)j].idx[hh];
+              if (t == 0x7fffffff) continue;
+              TriIsect T = S->isect[(size_t)t];
+              std::memcpy(&T.pad[0], &t, sizeof t);
+              S->bvh_wtris.push_back(T);
+            }
+          const int cnt = (int)S->bvh_wtris.size() - tfirst;
+          if (cnt < 1 || cnt > 16 || tfirst >= (1 << 26)) {
+            S->bvh_status = "leaf too large for the cooperative traversal";
+            return false;
+          }
+          ref = ~((tfirst << 4) | (cnt - 1));
+        }
+      } else {
+        for (int a = 0; a < 3; ++a) {  // empty slot: never hit
+          sl[a] = 1.f;
+          sl[3 + a] = -1.f;
+        }
+      }
+      std::memcpy(&sl[6], &ref, sizeof ref);
+    }
+    S->bvh_wide.push_back(W);
+  }
+  return true;
+}
+
 bool build_bvh(HostScene *S) {
   S->bvh_nodes.clear();
   S->bvh_pairs.clear();
@@ -406,6 +505,13 @@ bool build_bvh(HostScene *S) {
     std::memcpy(&N.q[3][0], kid, sizeof kid);
   }
   S->bvh_depth = B.max_depth;
+  if (!build_wide(S)) {
+    S->bvh_nodes.clear();
+    S->bvh_pairs.clear();
+    S->bvh_big_pairs.clear();
+    S->bvh_big_idx.clear();
+    return false;
+  }
   S->bvh_status = "ok";
   return true;
 }

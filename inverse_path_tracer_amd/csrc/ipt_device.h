@@ -589,6 +589,9 @@ __device__ __forceinline__ void bvh_big_pass(const BvhView &B, V3 p, V3 d, float
 // Slab form of a ray: t = fma(box, 1/d, -p/d) per axis; |d| < 2^-60 makes
 // that axis's parameters NaN, which min/max ignore (the slab is dropped:
 // conservative).  bvh.cpp states why the rounding of this form is covered.
+__device__ __forceinline__ int lane_rank64(uint64_t m) {  // set bits of m below this lane
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 struct SlabRay {
   f2 ix, iy, iz, ox, oy, oz;
 };
@@ -717,6 +720,175 @@ __device__ __forceinline__ int closest_hit_bvh(const BvhView &B, V3 p, V3 d, flo
   }
   best_t = bt;
   return bi;
+}
+
+// ------------------------------------------------------------ cooperative BVH traversal
+// The per-lane traversal above is latency-bound: the ~10% of lanes whose ray
+// reaches the tree each walk ~13 dependent node/leaf steps while the rest of
+// the wave idles.  Here the wave splits into 8 groups of 8 lanes and each
+// group carries ONE ray through an 8-wide tree (WideNode): lane j tests child
+// j's box, the group picks the nearest hit child with a DPP min-reduction and
+// pushes the others on a group stack in LDS; at a leaf lane j tests triangle
+// j and a lexicographic (t, index) DPP reduction merges the results.  About
+// 3 levels + a leaf or two instead of ~13 steps, 8 rays per wave per round.
+// All lanes of a group hold identical copies of the ray state, so every
+// branch is group-uniform and the DPP reductions (xor 1, xor 2 within quads,
+// half-row mirror) only read lanes of the same, active group.
+struct CoopView {
+  const float4 *wn;    // wide nodes: slot j of node n at wn[2 * (8 * n + j) + {0, 1}] (LDS or global)
+  const TriIsect *wt;  // leaf triangles, pad[0] = original index
+  uint32_t *stk;       // LDS: this wave's 8 group stacks, `stride` entries each
+  int stride;
+  float root[6];       // the tree's box: lo xyz, hi xyz
+};
+
+template <int CTRL>
+__device__ __forceinline__ void lexmin_dpp(float &t, int &i) {
+  const float t2 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(t), CTRL, 0xf, 0xf, false));
+  const int i2 = __builtin_amdgcn_update_dpp(0, i, CTRL, 0xf, 0xf, false);
+  const bool take = t2 < t || (t2 == t && i2 < i);
+  t = take ? t2 : t;
+  i = take ? i2 : i;
+}
+// Lexicographic minimum of (t, i) over the 8 lanes of each group.
+__device__ __forceinline__ void group_lexmin(float &t, int &i) {
+  lexmin_dpp<0xB1>(t, i);   // quad_perm [1,0,3,2]: partner lane ^ 1
+  lexmin_dpp<0x4E>(t, i);   // quad_perm [2,3,0,1]: partner lane ^ 2
+  lexmin_dpp<0x141>(t, i);  // row_half_mirror: lane 7 - i, the other quad of the group
+}
+__device__ __forceinline__ float bperm_f(int addr, float v) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v)));
+}
+
+// Does the ray reach the tree's box within [0, bt]?
+__device__ __forceinline__ bool coop_root_test(const CoopView &C, V3 p, V3 d, float bt) {
+  const SlabRay r = slab_ray(p, d);
+  const float tx0 = fmaf(C.root[0], r.ix.x, r.ox.x), tx1 = fmaf(C.root[3], r.ix.x, r.ox.x);
+  const float ty0 = fmaf(C.root[1], r.iy.x, r.oy.x), ty1 = fmaf(C.root[4], r.iy.x, r.oy.x);
+  const float tz0 = fmaf(C.root[2], r.iz.x, r.oz.x), tz1 = fmaf(C.root[5], r.iz.x, r.oz.x);
+  const float en = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.f));
+  const float ex = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), bt));
+  return en <= ex;
+}
+
+// The fp32 test of one triangle without the best-t condition (hit_test's
+// arithmetic): t if it accepts, +inf if not.
+__device__ __forceinline__ float tri_accept_t(const TriIsect &T, V3 p, V3 d) {
+  const float denom = fmaf(T.n[2], d.z, fmaf(T.n[1], d.y, T.n[0] * d.x));
+  const float px = p.x - T.c[0], py = p.y - T.c[1], pz = p.z - T.c[2];
+  const float num = fmaf(pz, T.n[2], fmaf(py, T.n[1], px * T.n[0]));
+  const float t = div_inrange(num, -denom);
+  const float qx = fmaf(d.x, t, p.x), qy = fmaf(d.y, t, p.y), qz = fmaf(d.z, t, p.z);
+  const float s0 = fmaf(qz, T.e0[2], fmaf(qy, T.e0[1], fmaf(qx, T.e0[0], T.e0[3])));
+  const float s1 = fmaf(qz, T.e1[2], fmaf(qy, T.e1[1], fmaf(qx, T.e1[0], T.e1[3])));
+  const float s2 = fmaf(qz, T.e2[2], fmaf(qy, T.e2[1], fmaf(qx, T.e2[0], T.e2[3])));
+  const bool ok = !(fabsf(denom) < kMinDotUp) && !(t < kEpsUp) && !(s0 > 0.f) && !(s1 > 0.f) && !(s2 > 0.f);
+  return ok ? t : __builtin_inff();
+}
+
+// Cooperative closest hit.  Called by ALL 64 lanes of the wave (convergent);
+// lanes with `need` have their (bt, bi) continued through the tree
+// lexicographically.  SHADOW: the entry bi is the target emitter; a group
+// stops as soon as its bi is no longer the target (occluded).
+template <bool SHADOW>
+__device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3 d, float &bt, int &bi) {
+  const int lane = (int)__lane_id();
+  const int g = lane >> 3, j = lane & 7;
+  uint64_t M = __ballot(need);
+  while (M) {
+    uint64_t Mr = M;  // the first (up to) 8 rays: group k takes the k-th
+    int src = -1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (Mr) {
+        const int idx = __builtin_ctzll(Mr);
+        Mr &= Mr - 1;
+        src = (g == k) ? idx : src;
+      }
+    }
+    const uint64_t taken = M & ~Mr;
+    M = Mr;
+    const int sa = (src < 0 ? lane : src) << 2;
+    const V3 gp = mk(bperm_f(sa, p.x), bperm_f(sa, p.y), bperm_f(sa, p.z));
+    const V3 gd = mk(bperm_f(sa, d.x), bperm_f(sa, d.y), bperm_f(sa, d.z));
+    float gt = bperm_f(sa, bt);
+    int gi = __builtin_amdgcn_ds_bpermute(sa, bi);
+    if (src >= 0) {
+      const int target = gi;
+      const SlabRay r = slab_ray(gp, gd);
+      uint32_t *stk = C.stk + g * C.stride;
+      int node = 0, sp = 0;
+#ifdef IPT_BVH_STATS
+      uint32_t st_nodes = 0, st_leaves = 0;
+#endif
+      for (;;) {
+        if (node >= 0) {  // wide node: lane j tests child j
+#ifdef IPT_BVH_STATS
+          ++st_nodes;
+#endif
+          const float4 a = C.wn[2 * (8 * node + j)], b = C.wn[2 * (8 * node + j) + 1];
+          const int ref = __float_as_int(b.z);
+          const float tx0 = fmaf(a.x, r.ix.x, r.ox.x), tx1 = fmaf(a.w, r.ix.x, r.ox.x);
+          const float ty0 = fmaf(a.y, r.iy.x, r.oy.x), ty1 = fmaf(b.x, r.iy.x, r.oy.x);
+          const float tz0 = fmaf(a.z, r.iz.x, r.oz.x), tz1 = fmaf(b.y, r.iz.x, r.oz.x);
+          const float en = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.f));
+          const float ex = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), gt));
+          const bool h = en <= ex && ref != kWideEmpty;
+          const uint32_t hm = (uint32_t)(__ballot(h) >> (lane & 56)) & 0xffu;
+          if (hm == 0) {
+            node = sp > 0 ? (int)stk[--sp] : kBvhDone;
+          } else {
+            float ek = h ? en : __builtin_inff();
+            int rk = h ? ref : 0x7fffffff;
+            group_lexmin(ek, rk);  // nearest hit child (ties: smaller ref)
+            const bool other = h && ref != rk;
+            const uint32_t om = (uint32_t)(__ballot(other) >> (lane & 56)) & 0xffu;
+            if (other) stk[sp + __popc(om & ((1u << j) - 1u))] = (uint32_t)ref;
+            sp += __popc(om);
+            node = rk;
+          }
+        } else {  // leaf: lane j tests triangle j (8 per round)
+#ifdef IPT_BVH_STATS
+          ++st_leaves;
+#endif
+          const int code = ~node;
+          const int first = code >> 4, cnt = (code & 15) + 1;
+          for (int base = 0; base < cnt; base += 8) {
+            float tj = __builtin_inff();
+            int ij = 0x7fffffff;
+            if (base + j < cnt) {
+              const TriIsect &T = C.wt[first + base + j];
+              tj = tri_accept_t(T, gp, gd);
+              ij = __float_as_int(T.pad[0]);
+            }
+            group_lexmin(tj, ij);
+            if (tj < gt || (tj == gt && ij < gi)) {
+              gt = tj;
+              gi = ij;
+            }
+          }
+          node = (SHADOW && gi != target) ? kBvhDone : (sp > 0 ? (int)stk[--sp] : kBvhDone);
+        }
+        if (node == kBvhDone) break;
+      }
+#ifdef IPT_BVH_STATS
+      if (j == 0) {
+        atomicAdd(&g_bvh_stats[0], 1ull);
+        atomicAdd(&g_bvh_stats[1], (unsigned long long)st_nodes);
+        atomicAdd(&g_bvh_stats[2], (unsigned long long)st_leaves);
+        if (SHADOW && gi != target) atomicAdd(&g_bvh_stats[3], 1ull);
+      }
+#endif
+    }
+    // results back to the owners: the ray of group k came from the k-th lane of `taken`
+    const int ra = (8 * lane_rank64(taken)) << 2;
+    const float rt = bperm_f(ra, gt);
+    const int ri = __builtin_amdgcn_ds_bpermute(ra, gi);
+    if ((taken >> lane) & 1ull) {
+      bt = rt;
+      bi = ri;
+    }
+  }
 }
 
 // Triangle::getNormal (scene_basics.h:100-109)

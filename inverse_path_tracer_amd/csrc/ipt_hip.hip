@@ -103,6 +103,12 @@ struct TraceArgs {
   // traversal stack entries per lane
   int bvh_lds_nodes, bvh_stack;
   int bvh_nbig;                 // large-triangle pairs tested before the traversal
+  // cooperative traversal (IPT_BVH_COOP): 8-wide nodes (first bvh_wide_lds of
+  // them staged in LDS: all or none), leaf triangles, group-stack entries
+  const WideNode *bvh_wide;
+  const TriIsect *bvh_wtris;
+  int bvh_wide_lds, coop_stride;
+  float root_box[6];
   const TriPair *bvh_big;
   const int32_t *bvh_big_idx;
   // ADJ gradient bins: grad_slots triangles accumulate in LDS fp64 (all of
@@ -161,6 +167,13 @@ constexpr int min_blocks() {
 #ifndef IPT_BVH_SERVER
 #define IPT_BVH_SERVER 0
 #endif
+// IPT_BVH_COOP=1 (default): the BVH instances traverse with 8-lane groups
+// over 8-wide nodes (ipt_device.h::coop_cast); 0: one lane per ray over the
+// binary tree (closest_hit_bvh).
+#ifndef IPT_BVH_COOP
+#define IPT_BVH_COOP 1
+#endif
+constexpr bool kCoop = IPT_BVH_COOP && !IPT_BVH_SERVER;
 constexpr int kBlockSrv = kBlock + 64;
 template <bool BVH>
 constexpr int block_threads() {
@@ -322,6 +335,12 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   bv.big_idx = nullptr;
   bv.big_e3 = nullptr;
   bv.nbig = 0;
+  CoopView cv;
+  cv.wn = nullptr;
+  cv.wt = a.bvh_wtris;
+  cv.stk = nullptr;
+  cv.stride = a.coop_stride;
+  for (int k = 0; k < 6; ++k) cv.root[k] = a.root_box[k];
   float *srvq = nullptr;  // SERVE: ray queue [kQFields][kQSlots]
   int *srvc = nullptr;    // SERVE: per path wave queued count [4], live flag [4]
   if (BVH) {
@@ -334,7 +353,14 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       for (int i = tid; i < 4 * a.bvh_lds_nodes; i += nthr) ln[i] = g[i];
       bv.lnodes = ln;
     }
-    float *be3 = reinterpret_cast<float *>(ln + 4 * a.bvh_lds_nodes);
+    float4 *lw = ln + 4 * a.bvh_lds_nodes;
+    cv.wn = reinterpret_cast<const float4 *>(a.bvh_wide);
+    if (kCoop && a.bvh_wide_lds > 0) {
+      const float4 *g = reinterpret_cast<const float4 *>(a.bvh_wide);
+      for (int i = tid; i < 16 * a.bvh_wide_lds; i += nthr) lw[i] = g[i];
+      cv.wn = lw;
+    }
+    float *be3 = reinterpret_cast<float *>(lw + 16 * a.bvh_wide_lds);
     for (int i = tid; i < 6 * a.bvh_nbig; i += nthr) {
       const int j = i / 6, kf = (i % 6) >> 1, h = i & 1;
       be3[i] = a.bvh_big[j].f[9 + 4 * kf][h];
@@ -348,6 +374,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       srvq = after;
       srvc = reinterpret_cast<int *>(srvq + kQFields * kQSlots);
       bv.stack = reinterpret_cast<uint32_t *>(srvc + 8) + (tid >= kBlock ? tid - kBlock : 0);  // stride 64
+    } else if (kCoop) {
+      cv.stk = reinterpret_cast<uint32_t *>(after) + (tid >> 6) * 8 * a.coop_stride;
     } else {
       bv.stack = reinterpret_cast<uint32_t *>(after) + tid;
     }
@@ -477,6 +505,13 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         t = srvq[6 * kQSlots + slot];
         hit = __float_as_int(srvq[7 * kQSlots + slot]);
       }
+    } else if (BVH && kCoop) {  // pre-pass per lane, the tree part by 8-lane groups
+      bool qn = false;
+      if (active) {
+        bvh_prepass<false>(bv, p, d, t, hit, -1);
+        qn = coop_root_test(cv, p, d, t);
+      }
+      coop_cast<false>(cv, qn, p, d, t, hit);
     } else if (active) {
       hit = cast<BVH>(isect, pairs, e3, nT, bv, p, d, t, -1);
     }
@@ -600,7 +635,13 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       }
     }
     if (__ballot(shadow)) {
-      if (!SERVE && shadow) hs = cast<BVH>(isect, pairs, e3, nT, bv, p, sd, ts, et);
+      if (BVH && kCoop) {
+        bool qn = false;
+        if (shadow && bvh_prepass<true>(bv, p, sd, ts, hs, et)) qn = coop_root_test(cv, p, sd, ts);
+        coop_cast<true>(cv, qn, p, sd, ts, hs);
+      } else if (!SERVE && shadow) {
+        hs = cast<BVH>(isect, pairs, e3, nT, bv, p, sd, ts, et);
+      }
       PHASE(3)
       if (shadow && hs == et) {  // must hit the sampled emitter itself
         const V3 ne = shading_normal(geom[et], along(p, sd, ts));
@@ -885,6 +926,8 @@ struct GpuScene {
   BvhPair *bpairs = nullptr;
   TriPair *big_pairs = nullptr;
   int32_t *big_idx = nullptr;
+  WideNode *wide = nullptr;
+  TriIsect *wtris = nullptr;
   int accel = IPT_ACCEL_AUTO;
   int *grad_map = nullptr, *slot_tri = nullptr;  // ADJ hot-set LDS slots (large scenes)
   int grid[12] = {0};       // resident workgroups per (mode, spec, bvh) (0 = not queried)
@@ -931,7 +974,8 @@ GpuScene *gpu_upload(const HostScene &host, std::string *err) {
   if (upload(&s->isect, host.isect) || upload(&s->pairs, pairs) || upload(&s->geom, host.geom) || upload(&s->mat, host.mat) ||
       upload(&s->kd, host.kd) || upload(&s->emit_tri, host.emit_tri) || upload(&s->emit_cdf, host.emit_cdf) ||
       upload(&s->emit_pmf, host.emit_pmf) || upload(&s->bnodes, host.bvh_nodes) || upload(&s->bpairs, host.bvh_pairs) ||
-      upload(&s->big_pairs, host.bvh_big_pairs) || upload(&s->big_idx, host.bvh_big_idx)) {
+      upload(&s->big_pairs, host.bvh_big_pairs) || upload(&s->big_idx, host.bvh_big_idx) ||
+      upload(&s->wide, host.bvh_wide) || upload(&s->wtris, host.bvh_wtris)) {
     *err = gpu_last_error();
     gpu_free(s);
     return nullptr;
@@ -985,6 +1029,8 @@ void gpu_free(GpuScene *s) {
   (void)hipFree(s->bpairs);
   (void)hipFree(s->big_pairs);
   (void)hipFree(s->big_idx);
+  (void)hipFree(s->wide);
+  (void)hipFree(s->wtris);
   (void)hipFree(s->grad_map);
   (void)hipFree(s->slot_tri);
   delete s;
@@ -1046,6 +1092,16 @@ static int resident_grid(GpuScene *s, size_t lds_bytes, int *grid) {
   return 0;
 }
 
+static TraceArgs make_args(const GpuScene *s, const RenderParams &p);
+static TraceArgs make_args_scene(const GpuScene *s) {
+  RenderParams p;
+  p.width = p.height = p.spp = 1;
+  p.max_bounces = 0;
+  p.seed = 0;
+  p.row_begin = 0;
+  p.row_end = 1;
+  return make_args(s, p);
+}
 static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   TraceArgs a;
   a.W = p.width;
@@ -1073,6 +1129,11 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.bvh_nbig = 0;
   a.bvh_big = nullptr;
   a.bvh_big_idx = nullptr;
+  a.bvh_wide = nullptr;
+  a.bvh_wtris = nullptr;
+  a.bvh_wide_lds = 0;
+  a.coop_stride = 0;
+  for (int k = 0; k < 6; ++k) a.root_box[k] = s->host.bvh_root_box[k];
   a.grad_slots = 0;
   a.grad_map = nullptr;
   a.slot_tri = nullptr;
@@ -1094,13 +1155,19 @@ static bool use_bvh(const GpuScene *s) {
 // stack per thread of a 256-thread block (the closest-hit probe).
 static size_t bvh_lds(const GpuScene *s, TraceArgs &a, size_t base, bool server) {
   const size_t nn = s->host.bvh_nodes.size();
-  a.bvh_lds_nodes = nn * sizeof(BvhNode) <= (size_t)kBvhLdsNodeBytes ? (int)nn : 0;
+  a.bvh_lds_nodes = (!kCoop && nn * sizeof(BvhNode) <= (size_t)kBvhLdsNodeBytes) ? (int)nn : 0;
+  const size_t nw = s->host.bvh_wide.size();
+  a.bvh_wide = s->wide;
+  a.bvh_wtris = s->wtris;
+  a.bvh_wide_lds = (kCoop && nw * sizeof(WideNode) <= (size_t)kBvhLdsNodeBytes) ? (int)nw : 0;
+  a.coop_stride = 7 * s->host.bvh_wdepth + 8;
   a.bvh_stack = std::max(1, s->host.bvh_depth);
   a.bvh_nbig = (int)s->host.bvh_big_pairs.size();
   a.bvh_big = s->big_pairs;
   a.bvh_big_idx = s->big_idx;
   const size_t head = bvh_lds_offset(base) + (size_t)a.bvh_lds_nodes * sizeof(BvhNode) +
-                      (size_t)a.bvh_nbig * 6 * sizeof(float);
+                      (size_t)a.bvh_wide_lds * sizeof(WideNode) + (size_t)a.bvh_nbig * 6 * sizeof(float);
+  if (kCoop) return head + (size_t)(kBlock / 64) * 8 * a.coop_stride * sizeof(uint32_t);
   if (server)
     return head + (size_t)kQFields * kQSlots * sizeof(float) + 8 * sizeof(int) + (size_t)a.bvh_stack * 64 * sizeof(uint32_t);
   return head + (size_t)a.bvh_stack * kBlock * sizeof(uint32_t);
@@ -1357,15 +1424,14 @@ template <bool BVH>
 __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__restrict__ isect,
                                                              const TriPair *__restrict__ pairs,
                                                              const BvhNode *__restrict__ bnodes,
-                                                             const BvhPair *__restrict__ bpairs, int nT, int small,
-                                                             int lds_nodes, const TriPair *__restrict__ big,
-                                                             const int32_t *__restrict__ big_idx, int nbig, int64_t n,
-                                                             const float *__restrict__ org,
+                                                             const BvhPair *__restrict__ bpairs, const TraceArgs a,
+                                                             int small, int64_t n, const float *__restrict__ org,
                                                              const float *__restrict__ dir,
                                                              const int *__restrict__ targets, float *__restrict__ t_out,
                                                              int *__restrict__ i_out) {
   extern __shared__ double lds[];
   const int tid = threadIdx.x;
+  const int nT = a.nT;
   const int nP = (nT + 1) >> 1;
   float *lds_e3 = reinterpret_cast<float *>(lds);
   const f2 *e3 = nullptr;
@@ -1386,35 +1452,70 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
   bv.big_idx = nullptr;
   bv.big_e3 = nullptr;
   bv.nbig = 0;
+  CoopView cv;
+  cv.wn = reinterpret_cast<const float4 *>(a.bvh_wide);
+  cv.wt = a.bvh_wtris;
+  cv.stk = nullptr;
+  cv.stride = a.coop_stride;
+  for (int k = 0; k < 6; ++k) cv.root[k] = a.root_box[k];
   if (BVH) {
     char *base = reinterpret_cast<char *>(lds);
     float4 *ln = reinterpret_cast<float4 *>(base + bvh_lds_offset((size_t)(small ? 6 * nP : 0) * sizeof(float)));
-    if (lds_nodes > 0) {
+    if (a.bvh_lds_nodes > 0) {
       const float4 *g = reinterpret_cast<const float4 *>(bnodes);
-      for (int i = tid; i < 4 * lds_nodes; i += kBlock) ln[i] = g[i];
+      for (int i = tid; i < 4 * a.bvh_lds_nodes; i += kBlock) ln[i] = g[i];
       bv.lnodes = ln;
     }
-    float *be3 = reinterpret_cast<float *>(ln + 4 * lds_nodes);
-    for (int i = tid; i < 6 * nbig; i += kBlock) {
-      const int j = i / 6, kf = (i % 6) >> 1, h = i & 1;
-      be3[i] = big[j].f[9 + 4 * kf][h];
+    float4 *lw = ln + 4 * a.bvh_lds_nodes;
+    if (kCoop && a.bvh_wide_lds > 0) {
+      const float4 *g = reinterpret_cast<const float4 *>(a.bvh_wide);
+      for (int i = tid; i < 16 * a.bvh_wide_lds; i += kBlock) lw[i] = g[i];
+      cv.wn = lw;
     }
-    bv.big = big;
-    bv.big_idx = big_idx;
+    float *be3 = reinterpret_cast<float *>(lw + 16 * a.bvh_wide_lds);
+    for (int i = tid; i < 6 * a.bvh_nbig; i += kBlock) {
+      const int j = i / 6, kf = (i % 6) >> 1, h = i & 1;
+      be3[i] = a.bvh_big[j].f[9 + 4 * kf][h];
+    }
+    bv.big = a.bvh_big;
+    bv.big_idx = a.bvh_big_idx;
     bv.big_e3 = reinterpret_cast<const f2 *>(be3);
-    bv.nbig = nbig;
-    bv.stack = reinterpret_cast<uint32_t *>(be3 + 6 * nbig) + tid;
+    bv.nbig = a.bvh_nbig;
+    uint32_t *after = reinterpret_cast<uint32_t *>(be3 + 6 * a.bvh_nbig);
+    if (kCoop) cv.stk = after + (tid >> 6) * 8 * a.coop_stride;
+    else bv.stack = after + tid;
   }
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * kBlock + tid;
-  if (i >= n) return;
-  const V3 p = mk(org[3 * i], org[3 * i + 1], org[3 * i + 2]);
-  const V3 d = mk(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);
-  const int target = targets ? targets[i] : -1;
+  const bool valid = i < n;  // no early return: the cooperative cast needs the whole wave
+  V3 p = mk(0.f, 0.f, 0.f), d = mk(0.f, 0.f, 1.f);
+  int target = -1;
+  if (valid) {
+    p = mk(org[3 * i], org[3 * i + 1], org[3 * i + 2]);
+    d = mk(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);
+    target = targets ? targets[i] : -1;
+  }
   float t = 0.f;
-  const int h = cast<BVH>(isect, pairs, e3, nT, bv, p, d, t, target);
-  t_out[i] = t;
-  i_out[i] = h;
+  int h = -1;
+  if (BVH && kCoop) {
+    bool qn = false;
+    if (valid) {
+      if (target >= 0) {
+        if (bvh_prepass<true>(bv, p, d, t, h, target)) qn = coop_root_test(cv, p, d, t);
+      } else {
+        bvh_prepass<false>(bv, p, d, t, h, -1);
+        qn = coop_root_test(cv, p, d, t);
+      }
+    }
+    coop_cast<false>(cv, qn && target < 0, p, d, t, h);
+    coop_cast<true>(cv, qn && target >= 0, p, d, t, h);
+  } else if (valid) {
+    h = cast<BVH>(isect, pairs, e3, nT, bv, p, d, t, target);
+  }
+  if (valid) {
+    t_out[i] = t;
+    i_out[i] = h;
+  }
 }
 
 int gpu_set_accel(GpuScene *s, int mode) {
@@ -1438,21 +1539,17 @@ int gpu_closest_hit(GpuScene *s, int64_t n, const float *org_dev, const float *d
     return -1;
   }
   if (n <= 0) return 0;
-  TraceArgs a;
-  std::memset(&a, 0, sizeof a);
-  a.nT = s->host.nT;
+  TraceArgs a = make_args_scene(s);
   const int small = (IPT_PAIRS && IPT_SMALL_UNROLL && s->host.nT <= 2 * kSmallPairs) ? 1 : 0;
   const size_t base = small ? (size_t)6 * ((s->host.nT + 1) / 2) * sizeof(float) : 0;
   const int blocks = (int)((n + kBlock - 1) / kBlock);
   if (use_bvh(s)) {
     const size_t lds = bvh_lds(s, a, base, false);
     hipLaunchKernelGGL(closest_hit_kernel<true>, dim3(blocks), dim3(kBlock), lds, (hipStream_t)stream, s->isect,
-                       s->pairs, s->bnodes, s->bpairs, s->host.nT, small, a.bvh_lds_nodes, a.bvh_big, a.bvh_big_idx,
-                       a.bvh_nbig, n, org_dev, dir_dev, targets_dev, t_dev, idx_dev);
+                       s->pairs, s->bnodes, s->bpairs, a, small, n, org_dev, dir_dev, targets_dev, t_dev, idx_dev);
   } else {
     hipLaunchKernelGGL(closest_hit_kernel<false>, dim3(blocks), dim3(kBlock), base, (hipStream_t)stream, s->isect,
-                       s->pairs, s->bnodes, s->bpairs, s->host.nT, small, 0, nullptr, nullptr, 0, n, org_dev, dir_dev,
-                       targets_dev, t_dev, idx_dev);
+                       s->pairs, s->bnodes, s->bpairs, a, small, n, org_dev, dir_dev, targets_dev, t_dev, idx_dev);
   }
   HIP_TRY(hipGetLastError());
   return 0;

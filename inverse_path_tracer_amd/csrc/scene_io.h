@@ -36,6 +36,11 @@ struct HostScene {
   // pairs in ascending original index, padded with zero triangles
   std::vector<TriPair> bvh_big_pairs;
   std::vector<int32_t> bvh_big_idx;  // 2 per pair; 0x7fffffff = padding
+  // the same tree collapsed to 8-wide nodes for the cooperative traversal
+  std::vector<WideNode> bvh_wide;   // breadth-first, root 0
+  std::vector<TriIsect> bvh_wtris;  // leaf triangles (pad[0] = original index)
+  int bvh_wdepth = 0;               // wide levels
+  float bvh_root_box[6] = {0, 0, 0, 0, 0, 0};  // lo xyz, hi xyz of the whole tree
   std::string bvh_status;      // "ok" or why the BVH was not built
 };
 

@@ -119,6 +119,19 @@ struct BvhPair {
 };
 static_assert(sizeof(BvhPair) == 160, "BvhPair layout");
 
+// 8-wide node of the cooperative traversal (ipt_device.h::coop_cast): one
+// 32-B slot per child -- lo.xyz, hi.xyz, ref, pad -- so lane j of an 8-lane
+// group reads its child with two 16-B loads, the group's eight reads being one
+// contiguous 256-B run.  ref >= 0: wide node; ref < 0: leaf, ~ref =
+// first_triangle << 4 | (count - 1) into the leaf-triangle array; kWideEmpty:
+// unused slot.  Leaf triangles are TriIsect records in leaf order with the
+// ORIGINAL triangle index in pad[0] (int bits).
+struct WideNode {
+  float s[8][8];
+};
+static_assert(sizeof(WideNode) == 256, "WideNode layout");
+constexpr int32_t kWideEmpty = (int32_t)0x80000000;
+
 // Device view of a loaded scene (all pointers are device pointers).
 struct DevScene {
   int nT, nE;
