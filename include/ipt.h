@@ -110,7 +110,8 @@ int ipt_scene_camera(void *scene, float *out16);
 #define IPT_ACCEL_BVH 2
 int ipt_scene_set_accel(void *scene, int mode);
 /* info8 = {nodes, leaf pairs, depth, accel in use (IPT_ACCEL_BRUTE/BVH),
- * large-triangle pairs tested before the traversal, 0, 0, 0}; returns 1 if
+ * large-triangle pairs tested before the traversal, 8-wide nodes, 8-wide
+ * levels, leaf triangles of the 8-wide tree}; returns 1 if
  * the scene has a BVH, 0 if not (ipt_last_error says why). */
 int ipt_scene_bvh_info(void *scene, int32_t *info8);
 /* nodes: info8[0]*16 floats (BvhNode), pairs: info8[1]*40 floats (BvhPair:

@@ -197,7 +197,9 @@ int ipt_scene_bvh_info(void *scene, int32_t *info8) {
   info8[2] = h.bvh_depth;
   info8[3] = ipt::gpu_accel_in_use(s);
   info8[4] = (int32_t)h.bvh_big_pairs.size();
-  info8[5] = info8[6] = info8[7] = 0;
+  info8[5] = (int32_t)h.bvh_wide.size();  // 8-wide nodes of the cooperative traversal
+  info8[6] = h.bvh_wdepth;
+  info8[7] = (int32_t)h.bvh_wtris.size();
   if (h.bvh_nodes.empty()) fail("no BVH: " + h.bvh_status);
   return h.bvh_nodes.empty() ? 0 : 1;
 }

@@ -74,7 +74,13 @@ constexpr int kMaxAdjTris = 65535;  // tri and et share one 32-bit field
 constexpr int kEdgeW = 8;      // graph bin: w, w*f, pix[3]*w*f, light[3]*w*f
 constexpr int kMaxAdjBounces = 62;
 constexpr int kMaxTableTris = 512;  // kd/kd-over-pi LDS tables up to 12 KB
-constexpr int kLdsGradBytes = 16 * 1024;  // ADJ gradient bins in LDS up to nT = 682
+#ifndef IPT_LDS_GRAD_KB
+#define IPT_LDS_GRAD_KB 12
+#endif
+// ADJ gradient bins in LDS (12 KB: all of them up to nT = 512, else the hot
+// set).  12 rather than 16 KB lets the BVH adjoint (bins + vertex records +
+// tree + group stacks) keep 3 workgroups per CU: sphere scene 16.3 -> 12.1 ms.
+constexpr int kLdsGradBytes = IPT_LDS_GRAD_KB * 1024;
 // Scenes of at least this many triangles trace through the BVH (auto mode).
 // Below it the unrolled / packed brute-force loop wins (a few pairs per cast).
 #ifndef IPT_BVH_MIN_TRIS
@@ -129,6 +135,16 @@ __device__ __forceinline__ uint64_t sample_pixel(const TraceArgs &a, uint64_t g)
   return a.idx32 ? (uint64_t)udiv32((uint32_t)g, a.m_spp, (uint32_t)a.spp) : g / (uint64_t)a.spp;
 }
 
+// pixel index of this launch's work item w (see the enumeration in trace_kernel)
+__device__ __forceinline__ uint64_t item_pixel(const TraceArgs &a, uint64_t w) {
+  if (!a.sample_major) return sample_pixel(a, a.s_begin + w);
+  if (a.idx32) {
+    const uint32_t sj = udiv32((uint32_t)w, a.m_npix, (uint32_t)a.npix);
+    return (uint64_t)((uint32_t)a.pix_begin + ((uint32_t)w - sj * (uint32_t)a.npix));
+  }
+  return a.pix_begin + (w - (w / a.npix) * a.npix);
+}
+
 using namespace dev;
 
 // ---------------------------------------------------------------------------
@@ -151,9 +167,16 @@ using namespace dev;
 #ifndef IPT_MIN_BLOCKS_BVH
 #define IPT_MIN_BLOCKS_BVH 4
 #endif
+// The adjoint's BVH instance: its LDS (gradient bins + vertex records + tree
+// + group stacks, ~55 KB for the sphere scene) allows only 2 workgroups per
+// CU, i.e. 2 waves/SIMD, so it may use up to 256 VGPRs without losing
+// residency (at 4 waves/SIMD it spilled).
+#ifndef IPT_MIN_BLOCKS_BVH_ADJ
+#define IPT_MIN_BLOCKS_BVH_ADJ 2
+#endif
 template <int MODE, bool BVH>
 constexpr int min_blocks() {
-  return BVH ? IPT_MIN_BLOCKS_BVH
+  return BVH ? (MODE == 1 ? IPT_MIN_BLOCKS_BVH_ADJ : IPT_MIN_BLOCKS_BVH)
              : (MODE == 0 ? IPT_MIN_BLOCKS_FWD : (MODE == 1 ? IPT_MIN_BLOCKS_ADJ : IPT_MIN_BLOCKS_GRAPH));
 }
 // IPT_BVH_SERVER=1: BVH instances run 4 path waves + 1 traversal-server
@@ -166,6 +189,17 @@ constexpr int min_blocks() {
 // frees were not the bottleneck.  Off by default.
 #ifndef IPT_BVH_SERVER
 #define IPT_BVH_SERVER 0
+#endif
+// Work enumeration of the adjoint and graph integrators.  Sample-major (1):
+// a wave's 64 lanes trace 64 different pixels, so their paths diverge at once
+// -- the LDS atomics of a vertex step hit different bins and few lanes of a
+// wave need the BVH tree in the same step; pixel-major (0): 64 samples of one
+// pixel, whose first vertices land on the same triangle (same bin).
+#ifndef IPT_ADJ_SAMPLE_MAJOR
+#define IPT_ADJ_SAMPLE_MAJOR 1
+#endif
+#ifndef IPT_GRAPH_SAMPLE_MAJOR
+#define IPT_GRAPH_SAMPLE_MAJOR 1
 #endif
 // IPT_BVH_COOP=1 (default): the BVH instances traverse with 8-lane groups
 // over 8-wide nodes (ipt_device.h::coop_cast); 0: one lane per ray over the
@@ -740,7 +774,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         const int K = k;
         if (K > 0) {
           const size_t fs = (size_t)vmax * kBlock;
-          const uint64_t pixel = sample_pixel(a, a.s_begin + witem);  // pixel-major
+          const uint64_t pixel = item_pixel(a, witem);
           const float ax = adj[pixel * 3 + 0] / (float)a.spp;
           const float ay = adj[pixel * 3 + 1] / (float)a.spp;
           const float az = adj[pixel * 3 + 2] / (float)a.spp;
@@ -1278,6 +1312,7 @@ int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const f
     return -1;
   }
   TraceArgs a = make_args(s, p);
+  a.sample_major = IPT_ADJ_SAMPLE_MAJOR;
   if (s->grad_map) {
     a.grad_slots = kLdsGradBytes / (3 * (int)sizeof(double));
     a.grad_map = s->grad_map;
@@ -1301,6 +1336,7 @@ int gpu_graph(GpuScene *s, const RenderParams &p, const uint8_t *target_dev, dou
   const size_t bins = (size_t)(s->host.nT + 1) * s->host.nT * kEdgeW * sizeof(double);
   a.lds_edges = bins <= 64 * 1024 ? 1 : 0;
   a.kd_tables = 0;  // the graph integrator never reads albedo
+  a.sample_major = IPT_GRAPH_SAMPLE_MAJOR;
   return launch<MODE_GRAPH>(s, a, (a.lds_edges ? bins : 0) + table_bytes(a), nullptr, nullptr, nullptr, nullptr, target_dev, acc_dev,
                             (hipStream_t)stream);
 }

@@ -155,6 +155,7 @@ class Scene:
         has = N.lib().ipt_scene_bvh_info(self.handle, info)
         N.check(has, "bvh_info")
         return {"has_bvh": bool(has), "nodes": info[0], "pairs": info[1], "depth": info[2], "big_pairs": info[4],
+                "wide_nodes": info[5], "wide_depth": info[6], "wide_tris": info[7],
                 "accel": {N.ACCEL_BRUTE: "brute", N.ACCEL_BVH: "bvh"}.get(info[3], "?"),
                 "status": "ok" if has else N.last_error()}
 

@@ -23,6 +23,13 @@ SCENES["scene0"] = SCENES["cornell"] + [(A + "/shapes/cube.obj", "*Kd 0.90414629
 if os.environ.get("IPT_VB_SPHERE"):  # large scene: BVH instance (triangle BVH + large-triangle pre-pass)
     SCENES["sphere"] = SCENES["cornell"] + [(A + "/shapes/sphere.obj", "*Kd 0.2 0.6 0.3*", (0.3, -1.2, 4.2), (0.0, 0.4, 0.0),
                                              (1.2, 1.2, 1.2))]
+if os.environ.get("IPT_VB_CLUTTER"):  # the 4-object scene of tests/test_bvh.py (2590 triangles)
+    SCENES["clutter"] = SCENES["cornell"] + [
+        (A + "/shapes/sphere.obj", "*Kd 0.2 0.6 0.3*", (0.3, -1.2, 4.2), (0.0, 0.4, 0.0), (1.2, 1.2, 1.2)),
+        (A + "/shapes/cube.obj", "*Kd 0.5 0.5 0.5*", (-0.9, -1.4, 3.9), (0.2, 0.7, 0.1), (0.7, 0.7, 0.7)),
+        (A + "/shapes/sphere.obj", "*Kd 0.9 0.1 0.1*", (0.8, 0.9, 4.6), (0.0, 0.0, 0.5), (0.5, 0.5, 0.5))]
+if os.environ.get("IPT_VB_ONLY"):  # comma-separated scene names
+    SCENES = {k: v for k, v in SCENES.items() if k in os.environ["IPT_VB_ONLY"].split(",")}
 
 
 def load(path):
