@@ -456,11 +456,20 @@ __device__ __forceinline__ int closest_hit_pairs_small(const TriPair *__restrict
   // of being hoisted out of the megakernel loop as SGPR masks (which spill)
   int nP = (nT + 1) >> 1;
   asm volatile("" : "+s"(nP));
+  // The LDS base of the plane offsets pinned in one VGPR for the whole cast:
+  // left alone, the compiler re-materialises it (a v_mov per pair, 1 of 46
+  // VALU) because a ds_read takes its address from a VGPR.
+  typedef __attribute__((address_space(3))) const f2 lds_f2;
+  lds_f2 *e3l = (lds_f2 *)e3;
+#ifndef IPT_PIN_E3
+#define IPT_PIN_E3 1
+#endif
+  if (IPT_PIN_E3) asm volatile("" : "+v"(e3l));
 #pragma unroll
   for (int j = 0; j < kSmallPairs; ++j) {
     if (j < nP) {  // wave-uniform
       const TriPair T = pairs[j];
-      pair_ray(T, pair_origin(T, p), 2 * j, 2 * j + 1, p, d, bt, bi, e3[3 * j], e3[3 * j + 1], e3[3 * j + 2]);
+      pair_ray(T, pair_origin(T, p), 2 * j, 2 * j + 1, p, d, bt, bi, e3l[3 * j], e3l[3 * j + 1], e3l[3 * j + 2]);
     }
   }
   best_t = bt;
