@@ -801,6 +801,9 @@ __device__ __forceinline__ float tri_accept_t(const TriIsect &T, V3 p, V3 d) {
 // stops as soon as its bi is no longer the target (occluded).
 template <bool SHADOW>
 __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3 d, float &bt, int &bi) {
+#ifdef IPT_ABL_NOTRAV  // timing-only ablation build: pre-pass only, no traversal
+  return;
+#endif
   const int lane = (int)__lane_id();
   const int g = lane >> 3, j = lane & 7;
   uint64_t M = __ballot(need);

@@ -1,0 +1,172 @@
+"""The reference workflow around the path tracer (SURVEY.md §8(f) rows 1 and
+4): dataset generation sharded over ranks (pipeline.py) and the DGL-free GCN
+(gcn.py, ipt.py:26-83)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from inverse_path_tracer_amd import gcn
+from inverse_path_tracer_amd import pipeline as P
+
+
+def _dense_propagate(w, pixel, h, p_min=gcn.P_MIN):
+    """ipt.py:68-83 + update_all as dense algebra: reduced = A @ h with
+    A[dst, src] = row-normalised kept weights (self loops filled with 0)."""
+    w = np.array(w, np.float64)
+    w[w < p_min] = 0
+    s = w.sum(-1, keepdims=True)
+    A = (w / np.where(s != 0, s, 1))[:-1]
+    return A @ h
+
+
+def _rand_graph_data(nT, rs):
+    w = rs.uniform(0, 1, (nT + 1, nT)) * (rs.uniform(size=(nT + 1, nT)) < 0.4)
+    w[rs.randint(0, nT + 1)] = 0  # an empty row (all weights dropped)
+    w[w < 2e-3] = 5e-4            # some entries below P_MIN
+    pixel = rs.uniform(0, 1, (nT + 1, nT, 3))
+    return w, pixel
+
+
+def test_build_graph_message_passing_matches_dense():
+    rs = np.random.RandomState(0)
+    for nT in (1, 7, 30):
+        w, pixel = _rand_graph_data(nT, rs)
+        w_in = w.copy()
+        g = gcn.build_graph(w, pixel, None)
+        assert np.array_equal(w, w_in)  # input not mutated
+        assert g.num_nodes == nT
+        np.testing.assert_allclose(g.node_feats.numpy(), pixel[-1], rtol=1e-7)
+        h = torch.from_numpy(rs.uniform(-1, 1, (nT, 5))).float()
+        got = g.propagate(h).double().numpy()
+        np.testing.assert_allclose(got, _dense_propagate(w, pixel, h.double().numpy()), rtol=1e-5, atol=1e-6)
+
+
+def test_self_loop_fill_one_adds_identity():
+    rs = np.random.RandomState(1)
+    w, pixel = _rand_graph_data(6, rs)
+    h = torch.from_numpy(rs.uniform(-1, 1, (6, 3))).float()
+    g0, g1 = gcn.build_graph(w, pixel), gcn.build_graph(w, pixel, self_loop_fill=1.0)
+    np.testing.assert_allclose((g1.propagate(h) - g0.propagate(h)).numpy(), h.numpy(), rtol=1e-6, atol=1e-6)
+
+
+def test_batch_is_block_diagonal():
+    rs = np.random.RandomState(2)
+    gs = [gcn.build_graph(*_rand_graph_data(n, rs)) for n in (3, 5, 4)]
+    b = gcn.batch(gs)
+    h = torch.randn(b.num_nodes, 4)
+    out, off = b.propagate(h), 0
+    for g in gs:
+        n = g.num_nodes
+        torch.testing.assert_close(out[off:off + n], g.propagate(h[off:off + n]))
+        off += n
+
+
+def test_gcn_shapes_and_training_reduces_loss():
+    rs = np.random.RandomState(3)
+    gs, ys = [], []
+    for _ in range(3):
+        w, pixel = _rand_graph_data(30, rs)
+        gs.append(gcn.build_graph(w, pixel))
+        ys.append(torch.from_numpy(pixel[-1] * 0.8 + 0.1))  # learnable target
+    m0 = gcn.GCN()
+    assert m0(gs[0]).shape == (30, 3)
+    torch.manual_seed(0)
+    x, y = gcn.batch(gs), torch.cat(ys).float()
+    first = float(gcn.GCN.loss(gcn.train(gs, ys, 0, lr=1e-3)(x), y).detach())
+    last = float(gcn.GCN.loss(gcn.train(gs, ys, 200, lr=1e-3)(x), y).detach())
+    assert last < 0.7 * first
+
+
+def test_scene_text_loads_like_scenes_0(tmp_path):
+    """generate_files' scene text (ipt_cuda.py:120-127) loads into the
+    reference's 30-triangle scene with the drawn cube Kd as its last 12 rows."""
+    from conftest import ASSETS
+    from inverse_path_tracer_amd.scene import Scene
+
+    kd = P.cube_kd(5, 17)
+    f = tmp_path / "s.txt"
+    f.write_text(P.scene_text(kd))
+    sc = Scene.from_file(str(f), root=ASSETS, device=False)
+    assert sc.nT == 30
+    np.testing.assert_array_equal(sc.materials[18:], np.tile(kd.astype(np.float32), (12, 1)))
+    assert all(0 <= v < 1 for v in kd)
+    assert not np.array_equal(P.cube_kd(5, 17), P.cube_kd(5, 18))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _files_worker(rank, world, port, root):
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.dirname(here))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from inverse_path_tracer_amd import pipeline
+
+    mine = pipeline.my_scenes(10, world, rank)
+
+    def stub(scene_file, i):  # stands in for the GPU render: the image encodes (rank, i)
+        return np.full((4, 6, 3), (rank, i, 7), np.uint8)
+
+    pipeline.generate_files(root, mine, seed=3, renderer=stub)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_generate_files_sharded_gloo(tmp_path):
+    """3 ranks write the 10 scenes round-robin: each file exactly once, by its
+    owner, and the scene files do not depend on the rank count."""
+    from inverse_path_tracer_amd.scene import png_read
+
+    root = str(tmp_path)
+    mp.spawn(_files_worker, args=(3, _free_port(), root), nprocs=3, join=True)
+    for i in range(10):
+        assert (tmp_path / "scenes" / ("%d.txt" % i)).read_text() == P.scene_text(P.cube_kd(3, i))
+        img = png_read(str(tmp_path / "imgs" / ("%d.png" % i)))
+        assert img.shape == (4, 6, 3) and tuple(img[0, 0]) == (i % 3, i, 7)
+    assert sorted(os.listdir(tmp_path / "scenes")) == sorted("%d.txt" % i for i in range(10))
+
+
+@pytest.mark.gpu
+def test_pipeline_end_to_end_gpu(tmp_path):
+    """files -> data -> train -> preds on the MI355X at a small size; the saved
+    graph equals a direct createGraph of the same scene, image and seed, and
+    the labels are the scene's materials."""
+    from inverse_path_tracer_amd.scene import Scene, compress, png_read, unpack_graph
+
+    root = str(tmp_path)
+    cfg = dict(width=24, height=16, spp=4, max_bounces=3, seed=11)
+    idx = [0, 1, 2]
+    P.generate_files(root, idx, **cfg)
+    P.generate_data(root, idx, **cfg)
+    data = P.load_data(root, idx)
+    for i, (w, pixel, light, labels) in zip(idx, data):
+        sc = Scene.from_file(os.path.join(root, "scenes", "%d.txt" % i), root=P.ASSETS)
+        target = png_read(os.path.join(root, "imgs", "%d.png" % i))
+        seed = P.scene_seed(11, i, 24, 16, 4) ^ 0x5bd1e995
+        acc, ref = sc.graph(target, 24, 16, 4, 3, seed)
+        np.testing.assert_array_equal(compress(sc.nT, acc), ref)
+        w2, p2, l2 = unpack_graph(sc.nT, ref)
+        np.testing.assert_array_equal(w, w2)
+        np.testing.assert_array_equal(pixel, p2)
+        np.testing.assert_array_equal(light, l2)
+        np.testing.assert_array_equal(labels, sc.materials.astype(np.float64))
+        _, ldr = sc.render(24, 16, 4, 3, P.scene_seed(11, i, 24, 16, 4), ldr=True)
+        np.testing.assert_array_equal(target, ldr)
+    _, errs = P.train_and_predict(root, idx, 20, lr=1e-3, device="cuda", **cfg)
+    assert len(errs) == 3 and all(np.isfinite(errs))
+    for i in idx:
+        assert png_read(os.path.join(root, "preds", "%d_pred.png" % i)).shape == (16, 24, 3)
+        assert os.path.exists(os.path.join(root, "preds", "%d_true.png" % i))
