@@ -174,9 +174,16 @@ using namespace dev;
 #ifndef IPT_MIN_BLOCKS_BVH_ADJ
 #define IPT_MIN_BLOCKS_BVH_ADJ 2
 #endif
+// The forward's BVH instance at 5 waves/SIMD (96 VGPRs, ~116 B of spill,
+// mostly outside the casts) beats 4 (121 VGPRs, none): sphere scene 9.92 ->
+// 9.48 ms (profiles/r01_variants_bvh_occupancy.log); 6 spills in the
+// traversal and loses (14.5 ms).
+#ifndef IPT_MIN_BLOCKS_BVH_FWD
+#define IPT_MIN_BLOCKS_BVH_FWD 5
+#endif
 template <int MODE, bool BVH>
 constexpr int min_blocks() {
-  return BVH ? (MODE == 1 ? IPT_MIN_BLOCKS_BVH_ADJ : IPT_MIN_BLOCKS_BVH)
+  return BVH ? (MODE == 1 ? IPT_MIN_BLOCKS_BVH_ADJ : (MODE == 0 ? IPT_MIN_BLOCKS_BVH_FWD : IPT_MIN_BLOCKS_BVH))
              : (MODE == 0 ? IPT_MIN_BLOCKS_FWD : (MODE == 1 ? IPT_MIN_BLOCKS_ADJ : IPT_MIN_BLOCKS_GRAPH));
 }
 // IPT_BVH_SERVER=1: BVH instances run 4 path waves + 1 traversal-server
