@@ -19,6 +19,19 @@
 namespace ipt {
 namespace dev {
 
+// Address-space-qualified views (LDS = 3, global = 1) for data that lives in
+// either place depending on the scene: separate typed accesses per branch
+// compile to ds_* / global_* instructions; one pointer that may be either
+// compiles to flat ones (vector-memory path and a vmcnt+lgkmcnt wait even
+// for LDS data), and LLVM merges untyped per-branch accesses back into one.
+typedef __attribute__((address_space(3))) float lds_f32;
+typedef __attribute__((address_space(3))) double lds_f64;
+typedef __attribute__((address_space(1))) float gbl_f32;
+typedef __attribute__((address_space(1))) double gbl_f64;
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4f lds_v4;
+typedef __attribute__((address_space(1))) v4f gbl_v4;
+
 // ------------------------------------------------------------ constants
 // scene_basics.h:13-14 compare a float against the double literals 1e-4 and
 // 1e-2.  For a float x, (double)x < 1e-4  <=>  x < kMinDotUp, where kMinDotUp
@@ -744,7 +757,8 @@ __device__ __forceinline__ int closest_hit_bvh(const BvhView &B, V3 p, V3 d, flo
 // branch is group-uniform and the DPP reductions (xor 1, xor 2 within quads,
 // half-row mirror) only read lanes of the same, active group.
 struct CoopView {
-  const float4 *wn;    // wide nodes: slot j of node n at wn[2 * (8 * n + j) + {0, 1}] (LDS or global)
+  const float4 *wn;    // wide nodes: slot j of node n at wn[2 * (8 * n + j) + {0, 1}]
+  bool wn_lds;         // wn points into LDS (else global memory)
   const TriIsect *wt;  // leaf triangles, pad[0] = original index
   uint32_t *stk;       // LDS: this wave's 8 group stacks, `stride` entries each
   int stride;
@@ -838,7 +852,18 @@ __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3
 #ifdef IPT_BVH_STATS
           ++st_nodes;
 #endif
-          const float4 a = C.wn[2 * (8 * node + j)], b = C.wn[2 * (8 * node + j) + 1];
+          float4 a, b;
+          if (C.wn_lds) {  // typed per branch: ds_read_b128, not a flat load
+            const lds_v4 *q = (const lds_v4 *)C.wn + 2 * (8 * node + j);
+            const v4f qa = q[0], qb = q[1];
+            a = make_float4(qa.x, qa.y, qa.z, qa.w);
+            b = make_float4(qb.x, qb.y, qb.z, qb.w);
+          } else {
+            const gbl_v4 *q = (const gbl_v4 *)C.wn + 2 * (8 * node + j);
+            const v4f qa = q[0], qb = q[1];
+            a = make_float4(qa.x, qa.y, qa.z, qa.w);
+            b = make_float4(qb.x, qb.y, qb.z, qb.w);
+          }
           const int ref = __float_as_int(b.z);
           const float tx0 = fmaf(a.x, r.ix.x, r.ox.x), tx1 = fmaf(a.w, r.ix.x, r.ox.x);
           const float ty0 = fmaf(a.y, r.iy.x, r.oy.x), ty1 = fmaf(b.x, r.iy.x, r.oy.x);

@@ -343,16 +343,26 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   // IEEE division the per-vertex code would do, instead of three divisions
   // per vertex.  Falls back to global memory for large scenes.
   float *tab = reinterpret_cast<float *>(lds + n_acc);
-  const float *kd_t = kd;   // kd[3*tri]
-  const float *kdpi_t = tab + 3 * nT;
   if (a.kd_tables) {
     for (int i = tid; i < 3 * nT; i += nthr) {
       const float v = kd[i];
       tab[i] = v;
       tab[3 * nT + i] = v / kPiF;
     }
-    kd_t = tab;
   }
+  // kd and kd/pi of triangle t, from the tables or from global memory by a
+  // wave-uniform branch (a pointer that may point at either compiles to flat
+  // loads: vector-memory latency and a vmcnt+lgkmcnt wait for LDS data)
+  const lds_f32 *tab_l = (const lds_f32 *)tab;
+  const gbl_f32 *kd_g = (const gbl_f32 *)kd;
+  auto kd3 = [&](int t) -> V3 {
+    if (a.kd_tables) return mk(tab_l[3 * t], tab_l[3 * t + 1], tab_l[3 * t + 2]);
+    return mk(kd_g[3 * t], kd_g[3 * t + 1], kd_g[3 * t + 2]);
+  };
+  auto kdpi3 = [&](int t) -> V3 {
+    if (a.kd_tables) return mk(tab_l[3 * nT + 3 * t], tab_l[3 * nT + 3 * t + 1], tab_l[3 * nT + 3 * t + 2]);
+    return mk(kd_g[3 * t] / kPiF, kd_g[3 * t + 1] / kPiF, kd_g[3 * t + 2] / kPiF);
+  };
   // edge-plane offsets of each triangle pair for the unrolled small-scene
   // closest-hit loop (ipt_device.h::closest_hit_pairs_small)
   const f2 *e3 = nullptr;
@@ -378,6 +388,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   bv.nbig = 0;
   CoopView cv;
   cv.wn = nullptr;
+  cv.wn_lds = false;
   cv.wt = a.bvh_wtris;
   cv.stk = nullptr;
   cv.stride = a.coop_stride;
@@ -400,6 +411,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       const float4 *g = reinterpret_cast<const float4 *>(a.bvh_wide);
       for (int i = tid; i < 16 * a.bvh_wide_lds; i += nthr) lw[i] = g[i];
       cv.wn = lw;
+      cv.wn_lds = true;
     }
     float *be3 = reinterpret_cast<float *>(lw + 16 * a.bvh_wide_lds);
     for (int i = tid; i < 6 * a.bvh_nbig; i += nthr) {
@@ -423,7 +435,21 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   }
   for (int i = tid; i < n_acc; i += nthr) lds_acc[i] = 0.0;
   __syncthreads();
-  double *acc = (MODE == MODE_GRAPH && !a.lds_edges) ? edges : lds_acc;
+  // fp64 bin updates go to LDS (ds_add_f64) or to global memory by a
+  // wave-uniform (GRAPH) or per-lane (ADJ hot set) branch -- never through
+  // one pointer that may be either: that compiles to flat atomics, which take
+  // the vector-memory path even when the address is in LDS.
+  // The pointers carry their address space in the type so that LLVM cannot
+  // merge the two branches' atomics back into one through a selected pointer.
+  auto bins_add = [&](bool in_lds, double *glob, size_t off, int n, const double *v) {
+    if (in_lds) {
+      lds_f64 *b = (lds_f64 *)lds_acc + off;
+      for (int i = 0; i < n; ++i) __hip_atomic_fetch_add(b + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+      gbl_f64 *b = (gbl_f64 *)glob + off;
+      for (int i = 0; i < n; ++i) __hip_atomic_fetch_add(b + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
 
   if (!SERVE || tid < kBlock) {  // path waves
   // wave-uniform sample range (static partition, regenerated per lane)
@@ -574,13 +600,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       const V3 q = along(p, d, t);
       if (MODE == MODE_GRAPH) {
         (void)uniform(st);  // isSpecular = u < P_SPEC(0), inv_path_trace.cu:117
-        double *e = acc + ((size_t)dst * nT + tri) * kEdgeW;  // Edge::update, inv_scene.h:26-36
-        const float wf = weight * 1.f;
-        atomicAdd(e + 0, (double)weight);
-        atomicAdd(e + 1, (double)wf);
-        atomicAdd(e + 2, (double)(wf * pix.x));
-        atomicAdd(e + 3, (double)(wf * pix.y));
-        atomicAdd(e + 4, (double)(wf * pix.z));
+        const float wf = weight * 1.f;  // Edge::update, inv_scene.h:26-36
+        const double v[5] = {(double)weight, (double)wf, (double)(wf * pix.x), (double)(wf * pix.y),
+                             (double)(wf * pix.z)};
+        bins_add(a.lds_edges != 0, edges, ((size_t)dst * nT + tri) * kEdgeW, 5, v);
       } else if (k == 0) {
         const TriMat &m = mat[tri];
         Le = mk(m.ke[0], m.ke[1], m.ke[2]);
@@ -692,16 +715,11 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           const TriMat &me = mat[et];
           if (MODE == MODE_GRAPH) {
             const float w2 = (float)(((double)((weight * ct) * ctp) / (td * td)) / (double)emit_pmf[emitter]);
-            double *e = acc + ((size_t)tri * nT + et) * kEdgeW;
             const float wf = w2 * kInvPiF;  // BSDF(direct) factor 1/pi, inv_path_trace.cu:8
-            atomicAdd(e + 0, (double)w2);
-            atomicAdd(e + 1, (double)wf);
-            atomicAdd(e + 2, (double)(wf * pix.x));
-            atomicAdd(e + 3, (double)(wf * pix.y));
-            atomicAdd(e + 4, (double)(wf * pix.z));
-            atomicAdd(e + 5, (double)(wf * me.ke[0]));
-            atomicAdd(e + 6, (double)(wf * me.ke[1]));
-            atomicAdd(e + 7, (double)(wf * me.ke[2]));
+            const double v[8] = {(double)w2, (double)wf, (double)(wf * pix.x), (double)(wf * pix.y),
+                                 (double)(wf * pix.z), (double)(wf * me.ke[0]), (double)(wf * me.ke[1]),
+                                 (double)(wf * me.ke[2])};
+            bins_add(a.lds_edges != 0, edges, ((size_t)tri * nT + et) * kEdgeW, 8, v);
           } else {
 #ifdef IPT_ABL_DP
             const float s = ((ct * ctp) / (ts * ts)) / emit_pmf[emitter];
@@ -713,12 +731,12 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             emit_et = et;
             const TriMat &m = mat[tri];
             if (SPEC && (m.flags & MAT_HAS_KS)) specd = phong(m.shininess, nh, din, sd);
-            const float *kdt = kd_t + 3 * tri;
+            const V3 kt = kd3(tri);
             if (SPEC)
-              Ld = mk((kdt[0] + m.ks[0] * specd) * lo.x, (kdt[1] + m.ks[1] * specd) * lo.y,
-                      (kdt[2] + m.ks[2] * specd) * lo.z);
+              Ld = mk((kt.x + m.ks[0] * specd) * lo.x, (kt.y + m.ks[1] * specd) * lo.y,
+                      (kt.z + m.ks[2] * specd) * lo.z);
             else  // Ks = 0: kd + 0*0 == kd
-              Ld = mk(kdt[0] * lo.x, kdt[1] * lo.y, kdt[2] * lo.z);
+              Ld = mk(kt.x * lo.x, kt.y * lo.y, kt.z * lo.z);
           }
         }
       }
@@ -752,9 +770,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       } else {
         L = mk(fmaf(M.x, Le.x + Ld.x, L.x), fmaf(M.y, Le.y + Ld.y, L.y), fmaf(M.z, Le.z + Ld.z, L.z));
         if (cont) {
-          const float *kp = a.kd_tables ? kdpi_t + 3 * tri : nullptr;
-          const float *kdt = kd_t + 3 * tri;
-          const float t0 = kp ? kp[0] : kdt[0] / kPiF, t1 = kp ? kp[1] : kdt[1] / kPiF, t2 = kp ? kp[2] : kdt[2] / kPiF;
+          const V3 tp = kdpi3(tri);
+          const float t0 = tp.x, t1 = tp.y, t2 = tp.z;
           if (SPEC) {
             const TriMat &m = mat[tri];
             M = mk((M.x * (t0 + m.ks[0] * speci)) * coeff, (M.y * (t1 + m.ks[1] * speci)) * coeff,
@@ -779,7 +796,11 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       } else if (MODE == MODE_ADJ) {
         // backward sweep over the recorded vertices (oracle adjoint_sample)
         const int K = k;
+#ifdef IPT_ABL_NOSWEEP  // timing-only ablation build: no backward sweep (no gradients)
+        if (0) {
+#else
         if (K > 0) {
+#endif
           const size_t fs = (size_t)vmax * kBlock;
           const uint64_t pixel = item_pixel(a, witem);
           const float ax = adj[pixel * 3 + 0] / (float)a.spp;
@@ -792,21 +813,16 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             return mk(me.ke[0] * es, me.ke[1] * es, me.ke[2] * es);
           };
           auto tdiff = [&](int tj, float si, float &x, float &y, float &z) {
-            if (a.kd_tables) {
-              const float *kp = kdpi_t + 3 * tj;
-              x = kp[0]; y = kp[1]; z = kp[2];
-            } else {
-              const float *kq = kd + 3 * tj;
-              x = kq[0] / kPiF; y = kq[1] / kPiF; z = kq[2] / kPiF;
-            }
+            const V3 tp = kdpi3(tj);
+            x = tp.x; y = tp.y; z = tp.z;
             if (SPEC) {
               const TriMat &mj = mat[tj];
               x = x + mj.ks[0] * si; y = y + mj.ks[1] * si; z = z + mj.ks[2] * si;
             }
           };
           auto ddir = [&](int tj, float sdj, float &x, float &y, float &z) {
-            const float *kq = kd_t + 3 * tj;
-            x = kq[0]; y = kq[1]; z = kq[2];
+            const V3 kt = kd3(tj);
+            x = kt.x; y = kt.y; z = kt.z;
             if (SPEC) {
               const TriMat &mj = mat[tj];
               x = x + mj.ks[0] * sdj; y = y + mj.ks[1] * sdj; z = z + mj.ks[2] * sdj;
@@ -828,6 +844,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             if (IPT_ADJ_STORE_M) {
               Mk = mk(r[kRecM * fs], r[(kRecM + 1) * fs], r[(kRecM + 2) * fs]);
             } else {
+#ifdef IPT_ABL_NOPREFIX  // timing-only ablation build: no prefix recompute (wrong gradients)
+              if (0)
+#endif
               for (int j = 0; j < kk; ++j) {
                 const float *rj = lds_rec + (size_t)j * kBlock + tid;
                 const float cj = rj[2 * fs];
@@ -851,10 +870,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             }
             {
               const int sl = a.grad_map ? a.grad_map[tk] : tk;
-              double *gb = sl >= 0 ? lds_acc + sl * 3 : grad + tk * 3;
-              atomicAdd(gb + 0, (double)(ax * gk.x));
-              atomicAdd(gb + 1, (double)(ay * gk.y));
-              atomicAdd(gb + 2, (double)(az * gk.z));
+              const double v[3] = {(double)(ax * gk.x), (double)(ay * gk.y), (double)(az * gk.z)};
+              bins_add(sl >= 0, grad, sl >= 0 ? (size_t)sl * 3 : (size_t)tk * 3, 3, v);
             }
             float dx, dy, dz, tx, ty, tz;
             ddir(tk, sdk, dx, dy, dz);
@@ -1497,6 +1514,7 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
   bv.nbig = 0;
   CoopView cv;
   cv.wn = reinterpret_cast<const float4 *>(a.bvh_wide);
+  cv.wn_lds = false;
   cv.wt = a.bvh_wtris;
   cv.stk = nullptr;
   cv.stride = a.coop_stride;
@@ -1514,6 +1532,7 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
       const float4 *g = reinterpret_cast<const float4 *>(a.bvh_wide);
       for (int i = tid; i < 16 * a.bvh_wide_lds; i += kBlock) lw[i] = g[i];
       cv.wn = lw;
+      cv.wn_lds = true;
     }
     float *be3 = reinterpret_cast<float *>(lw + 16 * a.bvh_wide_lds);
     for (int i = tid; i < 6 * a.bvh_nbig; i += kBlock) {
