@@ -197,6 +197,12 @@ constexpr int min_blocks() {
 #ifndef IPT_BVH_SERVER
 #define IPT_BVH_SERVER 0
 #endif
+// IPT_ADJ_WAVE_SWEEP=1: the adjoint's backward sweeps run as (path, vertex)
+// tasks spread over the whole wave (see trace_kernel); 0: each finishing lane
+// sweeps its own path.
+#ifndef IPT_ADJ_WAVE_SWEEP
+#define IPT_ADJ_WAVE_SWEEP 1
+#endif
 // Work enumeration of the adjoint and graph integrators.  Sample-major (1):
 // a wave's 64 lanes trace 64 different pixels, so their paths diverge at once
 // -- the LDS atomics of a vertex step hit different bins and few lanes of a
@@ -793,7 +799,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         o[0] = L.x;
         o[1] = L.y;
         o[2] = L.z;
-      } else if (MODE == MODE_ADJ) {
+      } else if (MODE == MODE_ADJ && !IPT_ADJ_WAVE_SWEEP) {
         // backward sweep over the recorded vertices (oracle adjoint_sample)
         const int K = k;
 #ifdef IPT_ABL_NOSWEEP  // timing-only ablation build: no backward sweep (no gradients)
@@ -878,6 +884,113 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             tdiff(tk, si, tx, ty, tz);
             S = mk((Le.x + dx * lk.x) + (tx * ck) * S.x, (Le.y + dy * lk.y) + (ty * ck) * S.y,
                    (Le.z + dz * lk.z) + (tz * ck) * S.z);
+          }
+        }
+      }
+    }
+    if (MODE == MODE_ADJ && IPT_ADJ_WAVE_SWEEP) {
+      // Wave-parallel sweep.  The vertices of the paths that finished in this
+      // iteration become tasks (path, vertex kk) spread over all 64 lanes:
+      // task kk recomputes its prefix throughput M_kk from records 0..kk-1
+      // and its suffix S_kk+1 from records kk+1..K-1 of the owner's LDS
+      // column with exactly the per-lane sweep's operations (the same floats;
+      // only the order of the fp64 gradient atomics changes), then adds its
+      // contribution.  The per-lane sweep ran on the ~1/3 of lanes whose path
+      // just ended while the rest idled.
+      const int Kf = (finished && k > 0) ? k : 0;
+      if (__ballot(Kf > 0)) {
+        const int lane = tid & 63;
+        int inc = Kf;  // inclusive scan of the task counts over the wave
+        for (int dd = 1; dd < 64; dd <<= 1) {
+          const int y = __shfl_up(inc, dd);
+          if (lane >= dd) inc += y;
+        }
+        const int T = __shfl(inc, 63);
+        float wx = 0.f, wy = 0.f, wz = 0.f;  // the owner's adjoint weights dL/dI / spp
+        if (Kf > 0) {
+          const uint64_t pixel = item_pixel(a, witem);
+          wx = adj[pixel * 3 + 0] / (float)a.spp;
+          wy = adj[pixel * 3 + 1] / (float)a.spp;
+          wz = adj[pixel * 3 + 2] / (float)a.spp;
+        }
+        const size_t fs = (size_t)vmax * kBlock;
+        for (int base = 0; base < T; base += 64) {
+          const int t = base + lane;
+          int ow = 0;  // owner lane: the smallest with inc > t
+          for (int step = 32; step >= 1; step >>= 1)
+            if (__shfl(inc, ow + step - 1) <= t) ow += step;
+          const int KL = __shfl(Kf, ow);
+          const int kk = t - (__shfl(inc, ow) - KL);
+          const bool esc = __shfl(escaped ? 1 : 0, ow) != 0;
+          const float ax = __shfl(wx, ow), ay = __shfl(wy, ow), az = __shfl(wz, ow);
+          const V3 LeL = mk(__shfl(Le.x, ow), __shfl(Le.y, ow), __shfl(Le.z, ow));
+          const V3 ML = mk(__shfl(M.x, ow), __shfl(M.y, ow), __shfl(M.z, ow));
+          if (t < T) {
+            const float *col = lds_rec + (tid & ~63) + ow;  // the owner's record column
+            auto rec_lo = [&](uint32_t f0, float es) {  // the forward's lo, same products
+              const TriMat &me = mat[f0 >> 16];
+              return mk(me.ke[0] * es, me.ke[1] * es, me.ke[2] * es);
+            };
+            auto tdiff = [&](int tj, const float *r) {  // T_j = kd/pi (+ Ks*speci)
+              V3 x = kdpi3(tj);
+              if (SPEC) {
+                const TriMat &mj = mat[tj];
+                const float si = r[(kRecSD + 1) * fs];
+                x = mk(x.x + mj.ks[0] * si, x.y + mj.ks[1] * si, x.z + mj.ks[2] * si);
+              }
+              return x;
+            };
+            auto ddir = [&](int tj, const float *r) {  // D_j = kd (+ Ks*specd)
+              V3 x = kd3(tj);
+              if (SPEC) {
+                const TriMat &mj = mat[tj];
+                const float sd = r[kRecSD * fs];
+                x = mk(x.x + mj.ks[0] * sd, x.y + mj.ks[1] * sd, x.z + mj.ks[2] * sd);
+              }
+              return x;
+            };
+            // suffix S_kk+1, built from the end exactly like the per-lane sweep
+            V3 S = mk(0.f, 0.f, 0.f);
+            if (esc) {
+              const float *r = col + (size_t)(KL - 1) * kBlock;
+              const uint32_t f0 = __float_as_uint(r[0]);
+              const V3 lk = rec_lo(f0, r[fs]);
+              const V3 dj = ddir((int)(f0 & 0xffffu), r);
+              S = mk(LeL.x + dj.x * lk.x, LeL.y + dj.y * lk.y, LeL.z + dj.z * lk.z);
+            }
+            for (int j = KL - 1; j > kk; --j) {
+              const float *r = col + (size_t)j * kBlock;
+              const uint32_t f0 = __float_as_uint(r[0]);
+              const int tj = (int)(f0 & 0xffffu);
+              const V3 lk = rec_lo(f0, r[fs]);
+              const float cj = r[2 * fs];
+              const V3 dj = ddir(tj, r), tjv = tdiff(tj, r);
+              S = mk((LeL.x + dj.x * lk.x) + (tjv.x * cj) * S.x, (LeL.y + dj.y * lk.y) + (tjv.y * cj) * S.y,
+                     (LeL.z + dj.z * lk.z) + (tjv.z * cj) * S.z);
+            }
+            // prefix throughput M_kk
+            V3 Mk = mk(1.f, 1.f, 1.f);
+            for (int j = 0; j < kk; ++j) {
+              const float *r = col + (size_t)j * kBlock;
+              const float cj = r[2 * fs];
+              const V3 tjv = tdiff((int)(__float_as_uint(r[0]) & 0xffffu), r);
+              Mk = mk((Mk.x * tjv.x) * cj, (Mk.y * tjv.y) * cj, (Mk.z * tjv.z) * cj);
+            }
+            const float *r = col + (size_t)kk * kBlock;
+            const uint32_t f0 = __float_as_uint(r[0]);
+            const int tk = (int)(f0 & 0xffffu);
+            const V3 lk = rec_lo(f0, r[fs]);
+            const float ck = r[2 * fs];
+            V3 dLd = Mk;
+            if (esc && kk == KL - 1) dLd = mk(dLd.x + ML.x, dLd.y + ML.y, dLd.z + ML.z);
+            V3 gk = mk(dLd.x * lk.x, dLd.y * lk.y, dLd.z * lk.z);
+            if (kk < KL - 1 || esc) {
+              const float cpi = ck / kPiF;
+              gk = mk(gk.x + (cpi * Mk.x) * S.x, gk.y + (cpi * Mk.y) * S.y, gk.z + (cpi * Mk.z) * S.z);
+            }
+            const int sl = a.grad_map ? a.grad_map[tk] : tk;
+            const double v[3] = {(double)(ax * gk.x), (double)(ay * gk.y), (double)(az * gk.z)};
+            bins_add(sl >= 0, grad, sl >= 0 ? (size_t)sl * 3 : (size_t)tk * 3, 3, v);
           }
         }
       }
