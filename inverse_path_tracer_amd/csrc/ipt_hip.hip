@@ -18,9 +18,11 @@
 //     ballot + mbcnt (wave-level compaction, no atomics), so lanes stay busy
 //     whatever the path-length spread (the reference's one-thread-per-sample
 //     launch idles a wave until its longest path ends);
-//   * every loop iteration casts exactly ONE ray per active lane (path rays
-//     and next-event shadow rays are phases of one state machine), so the
-//     dominant cost -- the closest-hit loop -- always runs with full waves;
+//   * one loop iteration is one path vertex for the whole wave, in
+//     wave-synchronous phases (path cast, shading with all of the vertex's
+//     random numbers, shadow cast, emitter term, finish), so each phase --
+//     above all the closest-hit loop -- runs once per iteration with most
+//     lanes on;
 //   * the closest-hit loop walks the triangle table with a wave-uniform
 //     index: 80-B records arrive through scalar loads and the test is
 //     branch-free per lane.
