@@ -99,6 +99,7 @@ struct TraceArgs {
   int lds_edges;  // GRAPH: bins privatised in LDS
   int sample_major;  // FWD: sample buffer [s][pixel][3] (else [pixel][s][3])
   int kd_tables;     // kd and kd/pi staged in LDS
+  const float *kdpi_g;  // kd/pi in global memory (large scenes: no LDS tables), per launch
   int small_pairs;   // nT <= 2*kSmallPairs: unrolled closest-hit, plane offsets in LDS
   uint64_t pix_begin, npix;
   // index arithmetic: when every global sample index of the frame is below
@@ -127,6 +128,9 @@ struct TraceArgs {
   const int *grad_map;
   const int *slot_tri;
   float cam[16];
+  // 1/spp when spp is a power of two (then x * rc_spp == x / spp for every
+  // float x: both are the correctly rounded x * 2^-k), else 0
+  float rc_spp;
 };
 
 __device__ __forceinline__ uint32_t udiv32(uint32_t n, uint64_t m, uint32_t d) {
@@ -369,7 +373,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   };
   auto kdpi3 = [&](int t) -> V3 {
     if (a.kd_tables) return mk(tab_l[3 * nT + 3 * t], tab_l[3 * nT + 3 * t + 1], tab_l[3 * nT + 3 * t + 2]);
-    return mk(kd_g[3 * t] / kPiF, kd_g[3 * t + 1] / kPiF, kd_g[3 * t + 2] / kPiF);
+    const gbl_f32 *q = (const gbl_f32 *)a.kdpi_g + 3 * t;
+    return mk(q[0], q[1], q[2]);
   };
   // edge-plane offsets of each triangle pair for the unrolled small-scene
   // closest-hit loop (ipt_device.h::closest_hit_pairs_small)
@@ -911,9 +916,15 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         float wx = 0.f, wy = 0.f, wz = 0.f;  // the owner's adjoint weights dL/dI / spp
         if (Kf > 0) {
           const uint64_t pixel = item_pixel(a, witem);
-          wx = adj[pixel * 3 + 0] / (float)a.spp;
-          wy = adj[pixel * 3 + 1] / (float)a.spp;
-          wz = adj[pixel * 3 + 2] / (float)a.spp;
+          if (a.rc_spp != 0.f) {
+            wx = adj[pixel * 3 + 0] * a.rc_spp;
+            wy = adj[pixel * 3 + 1] * a.rc_spp;
+            wz = adj[pixel * 3 + 2] * a.rc_spp;
+          } else {
+            wx = adj[pixel * 3 + 0] / (float)a.spp;
+            wy = adj[pixel * 3 + 1] / (float)a.spp;
+            wz = adj[pixel * 3 + 2] / (float)a.spp;
+          }
         }
         const size_t fs = (size_t)vmax * kBlock;
         for (int base = 0; base < T; base += 64) {
@@ -1094,6 +1105,7 @@ struct GpuScene {
   float *emit_cdf = nullptr, *emit_pmf = nullptr;
   float *ws = nullptr;  // per-sample radiance workspace
   size_t ws_bytes = 0;
+  float *kdpi = nullptr;  // kd / pi of the launch's albedo, when kd does not fit LDS tables
   bool has_ks = false;      // some material has a Phong lobe
   BvhNode *bnodes = nullptr;
   BvhPair *bpairs = nullptr;
@@ -1198,6 +1210,7 @@ void gpu_free(GpuScene *s) {
   (void)hipFree(s->emit_cdf);
   (void)hipFree(s->emit_pmf);
   (void)hipFree(s->ws);
+  (void)hipFree(s->kdpi);
   (void)hipFree(s->bnodes);
   (void)hipFree(s->bpairs);
   (void)hipFree(s->big_pairs);
@@ -1288,6 +1301,7 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.nE = s->host.nE;
   a.lds_edges = 0;
   a.sample_major = 0;
+  a.kdpi_g = nullptr;
   a.kd_tables = s->host.nT <= kMaxTableTris ? 1 : 0;
   a.small_pairs = (IPT_PAIRS && IPT_SMALL_UNROLL && s->host.nT <= 2 * kSmallPairs) ? 1 : 0;
   a.pix_begin = (uint64_t)p.row_begin * p.width;
@@ -1311,6 +1325,7 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.grad_map = nullptr;
   a.slot_tri = nullptr;
   std::memcpy(a.cam, s->host.cam, sizeof a.cam);
+  a.rc_spp = (p.spp > 0 && p.spp <= (1 << 24) && (p.spp & (p.spp - 1)) == 0) ? 1.0f / (float)p.spp : 0.f;
   return a;
 }
 
@@ -1372,9 +1387,24 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
 // instance, used when some material has Ks != 0; the shipped scenes have
 // none, and dropping the code lowers register pressure (occupancy).  The BVH
 // instances carry the traversal (and its LDS) only for large scenes.
+// kd / pi once per launch for scenes without LDS tables (the same IEEE
+// division the per-vertex code would do three times per vertex)
+__global__ __launch_bounds__(kBlock) void kdpi_kernel(const float *__restrict__ kd, int n, float *__restrict__ out) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) out[i] = kd[i] / kPiF;
+}
+
 template <int MODE>
 static int launch(GpuScene *s, TraceArgs a, size_t lds, const float *kd_dev, float *out, const float *adj,
                   double *grad, const uint8_t *target, double *edges, hipStream_t st) {
+  if (MODE != MODE_GRAPH && !a.kd_tables && a.n_samples > 0) {
+    const int n = 3 * s->host.nT;
+    if (!s->kdpi) HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s->kdpi), (size_t)n * sizeof(float)));
+    hipLaunchKernelGGL(kdpi_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, kd_dev ? kd_dev : s->kd, n,
+                       s->kdpi);
+    HIP_TRY(hipGetLastError());
+    a.kdpi_g = s->kdpi;
+  }
   if (use_bvh(s)) {
     lds = bvh_lds(s, a, lds, IPT_BVH_SERVER != 0);
     if (s->has_ks) return launch_inst<MODE, true, true>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
