@@ -595,15 +595,23 @@ __device__ __forceinline__ void bvh_pair_test(const BvhPair &T, V3 p, V3 d, floa
 
 // The large triangles, unrolled like closest_hit_pairs_small (scalar-loaded
 // pairs, plane offsets from LDS) with the lexicographic accept.
+// LEX = false is exact only from the empty state (bt = inf): the pairs come
+// in ascending original index, so the strict in-order accept is then already
+// the lexicographic minimum (2-3 fewer VALU per triangle); the shadow
+// pre-pass starts from the target's (t, index) and needs LEX.
+template <bool LEX>
 __device__ __forceinline__ void bvh_big_pass(const BvhView &B, V3 p, V3 d, float &bt, int &bi) {
   int nP = B.nbig;
   asm volatile("" : "+s"(nP));
+  typedef __attribute__((address_space(3))) const f2 lds_f2;  // LDS base pinned in a VGPR (see closest_hit_pairs_small)
+  lds_f2 *e3l = (lds_f2 *)B.big_e3;
+  if (IPT_PIN_E3) asm volatile("" : "+v"(e3l));
 #pragma unroll
   for (int j = 0; j < kSmallPairs; ++j) {
     if (j < nP) {  // wave-uniform
       const TriPair T = B.big[j];
-      pair_ray<true>(T, pair_origin(T, p), B.big_idx[2 * j], B.big_idx[2 * j + 1], p, d, bt, bi, B.big_e3[3 * j],
-                     B.big_e3[3 * j + 1], B.big_e3[3 * j + 2]);
+      pair_ray<LEX>(T, pair_origin(T, p), B.big_idx[2 * j], B.big_idx[2 * j + 1], p, d, bt, bi, e3l[3 * j],
+                    e3l[3 * j + 1], e3l[3 * j + 2]);
     }
   }
 }
@@ -658,7 +666,7 @@ __device__ __forceinline__ bool bvh_prepass(const BvhView &B, V3 p, V3 d, float 
     if (bi < 0) return false;  // the target itself is missed: not the closest hit either
   }
   if (B.nbig > 0) {
-    bvh_big_pass(B, p, d, bt, bi);
+    bvh_big_pass<SHADOW>(B, p, d, bt, bi);
     if (SHADOW && bi != target) return false;  // occluded by a large triangle: decided
   }
   return true;
