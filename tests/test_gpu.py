@@ -131,7 +131,9 @@ def test_row_band_sharding_bit_exact(scenes, W, H, spp, mb, world):
 
 # ------------------------------------------------------------- adjoint
 @pytest.mark.parametrize("name,W,H,spp,mb,seed", [
-    ("scene0", 64, 64, 8, 4, 3), ("scene0", 31, 23, 4, 8, 1), ("cornell", 48, 48, 8, 2, 6), ("scene0", 16, 16, 4, 0, 2)])
+    ("scene0", 64, 64, 8, 4, 3), ("scene0", 31, 23, 4, 8, 1), ("cornell", 48, 48, 8, 2, 6), ("scene0", 16, 16, 4, 0, 2),
+    # spp not a power of two (the weight division path), long paths (many sweep tasks per lane)
+    ("scene0", 20, 12, 3, 5, 5), ("cornell", 24, 16, 5, 20, 7)])
 def test_adjoint_matches_oracle(scenes, name, W, H, spp, mb, seed):
     P, Q = scenes[name]
     adj = np.random.RandomState(seed).uniform(-1, 1, (H, W, 3)).astype(np.float32)
