@@ -8,6 +8,6 @@ for set in "VALUBusy" "VALUUtilization" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SM
            "SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc $set -d $OUT/${T}_$i -o run --output-format csv \
-      -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/${T}_$i.log 2>&1 || { echo "fail $i" > $OUT/${T}.status; exit 1; }
+      -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-secondary > $OUT/${T}_$i.log 2>&1 || { echo "fail $i" > $OUT/${T}.status; exit 1; }
 done
 echo ok > $OUT/${T}.status
