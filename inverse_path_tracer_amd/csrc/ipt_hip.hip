@@ -153,6 +153,40 @@ __device__ __forceinline__ uint64_t item_pixel(const TraceArgs &a, uint64_t w) {
 
 using namespace dev;
 
+// Work item w of a launch -> global sample g, pixel (r, c), XORWOW state
+// after the two camera draws and the camera ray (path_trace.cu:150-165); the
+// enumeration is described in trace_kernel.
+__device__ __forceinline__ void item_ray(const TraceArgs &a, uint64_t w, Rng &st, V3 &p, V3 &d, int &r, int &c) {
+  uint64_t g;
+  if (a.idx32) {
+    uint32_t pixel;
+    if (a.sample_major) {
+      const uint32_t sj = udiv32((uint32_t)w, a.m_npix, (uint32_t)a.npix);
+      pixel = (uint32_t)a.pix_begin + ((uint32_t)w - sj * (uint32_t)a.npix);
+      g = (uint64_t)pixel * (uint32_t)a.spp + sj;
+    } else {
+      g = a.s_begin + w;
+      pixel = udiv32((uint32_t)g, a.m_spp, (uint32_t)a.spp);
+    }
+    r = (int)udiv32(pixel, a.m_W, (uint32_t)a.W);
+    c = (int)(pixel - (uint32_t)r * (uint32_t)a.W);
+  } else {
+    uint64_t pixel;
+    if (a.sample_major) {
+      const uint64_t sj = w / a.npix;
+      pixel = a.pix_begin + (w - sj * a.npix);
+      g = pixel * (uint64_t)a.spp + sj;
+    } else {
+      g = a.s_begin + w;
+      pixel = g / (uint64_t)a.spp;
+    }
+    r = (int)(pixel / (uint64_t)a.W);
+    c = (int)(pixel % (uint64_t)a.W);
+  }
+  rng_init(st, a.seed + g);
+  camera_ray(a.cam, st, r, c, a.W, a.H, p, d);
+}
+
 // ---------------------------------------------------------------------------
 // Minimum resident 256-thread blocks per CU (= waves per SIMD) requested per
 // integrator; 0 lets the compiler choose.  Measured (profiles/
@@ -209,6 +243,19 @@ constexpr int min_blocks() {
 #ifndef IPT_ADJ_WAVE_SWEEP
 #define IPT_ADJ_WAVE_SWEEP 1
 #endif
+// IPT_RAY_RING=1: camera rays come from a per-wave LDS ring filled 64 at a
+// time (trace_kernel).  Brute-force adjoint only: C2 adjoint 3.01 -> 2.95 ms,
+// C3 3.93 -> 3.87 (profiles/r01_variants_ray_ring.log); the forward measured
+// no change (and spills 20 B more with it); the BVH instances' LDS is spoken
+// for; the graph also needs the target pixel.
+#ifndef IPT_RAY_RING
+#define IPT_RAY_RING 1
+#endif
+constexpr int kRingFields = 9;  // d.xyz, XORWOW d, v0..v4
+template <int MODE, bool BVH>
+constexpr bool ring_on() {
+  return IPT_RAY_RING && !BVH && MODE == 1;
+}
 // Work enumeration of the adjoint and graph integrators.  Sample-major (1):
 // a wave's 64 lanes trace 64 different pixels, so their paths diverge at once
 // -- the LDS atomics of a vertex step hit different bins and few lanes of a
@@ -389,6 +436,14 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     e3 = reinterpret_cast<const f2 *>(lds_e3);
   }
   float *lds_rec = lds_e3 + (a.small_pairs ? 6 * nP : 0);
+  // Camera-ray ring (RING instances): per wave kRingFields x 64 words after the
+  // ADJ records, then the camera origin (3 floats per wave).
+  constexpr bool RING = ring_on<MODE, BVH>();
+  float *ring = nullptr;
+  if (RING) {
+    const size_t rec_words = (MODE == MODE_ADJ) ? (size_t)vmax * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock : 0;
+    ring = lds_rec + rec_words + (size_t)(tid >> 6) * (kRingFields * 64 + 4);
+  }
   BvhView bv;
   bv.nodes = bnodes;
   bv.pairs = bpairs;
@@ -498,9 +553,69 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   uint64_t tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t tp_ = __builtin_amdgcn_s_memtime();
 #endif
+  // RING: the wave's camera rays are generated 64 at a time by all lanes
+  // (index math, XORWOW init, the two camera draws, camera_ray) into an LDS
+  // ring, and a lane that needs a new path pops the next one: the same work
+  // items in the same order as the per-lane refill below, computed at full
+  // lane utilisation instead of by the ~1/3 of lanes that finished.
+  uint64_t ring_w = 0;  // work item of ring slot 0
+  int ring_n = 0, ring_h = 0;  // slots left, next slot
+  const int lane = tid & 63;
   for (;;) {
+    if (RING) {
+      uint64_t need = __ballot(!active);
+      int n_need = __popcll(need);
+      uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+      while (n_need > 0 && (ring_n > 0 || next < end)) {  // wave-uniform
+        if (ring_n == 0) {
+          const uint64_t w = next + (uint64_t)lane;
+          if (w < end) {
+            Rng s2;
+            V3 p2, d2;
+            int r2, c2;
+            item_ray(a, w, s2, p2, d2, r2, c2);
+            float *q = ring + lane;
+            q[0] = d2.x; q[64] = d2.y; q[128] = d2.z;
+            q[192] = __uint_as_float(s2.d); q[256] = __uint_as_float(s2.v0); q[320] = __uint_as_float(s2.v1);
+            q[384] = __uint_as_float(s2.v2); q[448] = __uint_as_float(s2.v3); q[512] = __uint_as_float(s2.v4);
+            if (lane == 0) {
+              ring[kRingFields * 64 + 0] = p2.x;
+              ring[kRingFields * 64 + 1] = p2.y;
+              ring[kRingFields * 64 + 2] = p2.z;
+            }
+          }
+          const uint64_t left = end - next;
+          ring_w = next;
+          ring_n = left < 64 ? (int)left : 64;
+          ring_h = 0;
+          next += (uint64_t)ring_n;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // ring writes before the pops below
+          __builtin_amdgcn_wave_barrier();
+        }
+        const int take = n_need < ring_n ? n_need : ring_n;
+        if (!active && (int)rank < take) {
+          const int slot = ring_h + (int)rank;
+          const float *q = ring + slot;
+          witem = ring_w + (uint64_t)slot;
+          d = mk(q[0], q[64], q[128]);
+          st.d = __float_as_uint(q[192]); st.v0 = __float_as_uint(q[256]); st.v1 = __float_as_uint(q[320]);
+          st.v2 = __float_as_uint(q[384]); st.v3 = __float_as_uint(q[448]); st.v4 = __float_as_uint(q[512]);
+          p = mk(ring[kRingFields * 64 + 0], ring[kRingFields * 64 + 1], ring[kRingFields * 64 + 2]);
+          L = mk(0.f, 0.f, 0.f);
+          Le = L;
+          Ld = L;
+          M = mk(1.f, 1.f, 1.f);
+          k = 0;
+          active = true;
+        }
+        rank -= (uint32_t)take;  // lanes still waiting move up
+        ring_h += take;
+        ring_n -= take;
+        n_need -= take;
+      }
+    }
     // ---- refill finished lanes from the wave's range (ballot + mbcnt)
-    const uint64_t need = __ballot(!active);
+    const uint64_t need = RING ? 0ull : __ballot(!active);
     if (need) {
       const uint32_t rank =
           __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
@@ -508,35 +623,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         const uint64_t w = next + rank;
         if (w < end) {
           witem = w;
-          uint64_t g;
           int r, c;
-          if (a.idx32) {
-            uint32_t pixel;
-            if (a.sample_major) {
-              const uint32_t sj = udiv32((uint32_t)w, a.m_npix, (uint32_t)a.npix);
-              pixel = (uint32_t)a.pix_begin + ((uint32_t)w - sj * (uint32_t)a.npix);
-              g = (uint64_t)pixel * (uint32_t)a.spp + sj;
-            } else {
-              g = a.s_begin + w;
-              pixel = udiv32((uint32_t)g, a.m_spp, (uint32_t)a.spp);
-            }
-            r = (int)udiv32(pixel, a.m_W, (uint32_t)a.W);
-            c = (int)(pixel - (uint32_t)r * (uint32_t)a.W);
-          } else {
-            uint64_t pixel;
-            if (a.sample_major) {
-              const uint64_t sj = w / a.npix;
-              pixel = a.pix_begin + (w - sj * a.npix);
-              g = pixel * (uint64_t)a.spp + sj;
-            } else {
-              g = a.s_begin + w;
-              pixel = g / (uint64_t)a.spp;
-            }
-            r = (int)(pixel / (uint64_t)a.W);
-            c = (int)(pixel % (uint64_t)a.W);
-          }
-          rng_init(st, a.seed + g);
-          camera_ray(a.cam, st, r, c, a.W, a.H, p, d);
+          item_ray(a, w, st, p, d, r, c);
           L = mk(0.f, 0.f, 0.f);
           Le = L;
           Ld = L;
@@ -1405,6 +1493,8 @@ static int launch(GpuScene *s, TraceArgs a, size_t lds, const float *kd_dev, flo
     HIP_TRY(hipGetLastError());
     a.kdpi_g = s->kdpi;
   }
+  if (!use_bvh(s) && ring_on<MODE, false>())  // camera-ray rings after the records
+    lds += (size_t)(kBlock / 64) * (kRingFields * 64 + 4) * sizeof(float);
   if (use_bvh(s)) {
     lds = bvh_lds(s, a, lds, IPT_BVH_SERVER != 0);
     if (s->has_ks) return launch_inst<MODE, true, true>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
