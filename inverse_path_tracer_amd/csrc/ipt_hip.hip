@@ -131,6 +131,7 @@ struct TraceArgs {
   // 1/spp when spp is a power of two (then x * rc_spp == x / spp for every
   // float x: both are the correctly rounded x * 2^-k), else 0
   float rc_spp;
+  int use_ring;  // RING instances: camera rays from the LDS ring (host decides: only if it costs no residency)
 };
 
 __device__ __forceinline__ uint32_t udiv32(uint32_t n, uint64_t m, uint32_t d) {
@@ -438,7 +439,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   float *lds_rec = lds_e3 + (a.small_pairs ? 6 * nP : 0);
   // Camera-ray ring (RING instances): per wave kRingFields x 64 words after the
   // ADJ records, then the camera origin (3 floats per wave).
-  constexpr bool RING = ring_on<MODE, BVH>();
+  const bool RING = ring_on<MODE, BVH>() && a.use_ring;
   float *ring = nullptr;
   if (RING) {
     const size_t rec_words = (MODE == MODE_ADJ) ? (size_t)vmax * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock : 0;
@@ -1413,6 +1414,7 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.grad_map = nullptr;
   a.slot_tri = nullptr;
   std::memcpy(a.cam, s->host.cam, sizeof a.cam);
+  a.use_ring = 0;
   a.rc_spp = (p.spp > 0 && p.spp <= (1 << 24) && (p.spp & (p.spp - 1)) == 0) ? 1.0f / (float)p.spp : 0.f;
   return a;
 }
@@ -1493,8 +1495,16 @@ static int launch(GpuScene *s, TraceArgs a, size_t lds, const float *kd_dev, flo
     HIP_TRY(hipGetLastError());
     a.kdpi_g = s->kdpi;
   }
-  if (!use_bvh(s) && ring_on<MODE, false>())  // camera-ray rings after the records
-    lds += (size_t)(kBlock / 64) * (kRingFields * 64 + 4) * sizeof(float);
+  a.use_ring = 0;
+  if (!use_bvh(s) && ring_on<MODE, false>()) {  // camera-ray rings after the records, if residency allows
+    const size_t ring = (size_t)(kBlock / 64) * (kRingFields * 64 + 4) * sizeof(float);
+    const size_t cap = 160 * 1024, want = (size_t)min_blocks<MODE, false>();
+    const size_t without = std::min(want, cap / std::max<size_t>(lds, 1)), with = std::min(want, cap / (lds + ring));
+    if (with >= without) {
+      a.use_ring = 1;
+      lds += ring;
+    }
+  }
   if (use_bvh(s)) {
     lds = bvh_lds(s, a, lds, IPT_BVH_SERVER != 0);
     if (s->has_ks) return launch_inst<MODE, true, true>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
