@@ -74,6 +74,14 @@ constexpr int kRecFieldsDiffuse = IPT_ADJ_STORE_M ? 6 : 3;
 constexpr int kRecFieldsSpec = kRecFieldsDiffuse + 2;
 constexpr int kMaxAdjTris = 65535;  // tri and et share one 32-bit field
 constexpr int kEdgeW = 8;      // graph bin: w, w*f, pix[3]*w*f, light[3]*w*f
+// LDS form of the graph bins: 5 doubles per (dst, src) (w, w*f, pix[3]*w*f)
+// plus 3 light doubles per (dst, emitter) -- only next-event updates, whose
+// source is an emitter, touch the light fields.  60 -> 39 KB for scenes/0.txt
+// (2 -> 4 workgroups per CU); flushed into the global kEdgeW-wide layout.
+constexpr int kEdgeL = 5;
+__host__ __device__ inline size_t graph_lds_doubles(int nT, int nE) {
+  return (size_t)(nT + 1) * nT * kEdgeL + (size_t)(nT + 1) * (nE > 0 ? nE : 0) * 3;
+}
 constexpr int kMaxAdjBounces = 62;
 constexpr int kMaxTableTris = 512;  // kd/kd-over-pi LDS tables up to 12 KB
 #ifndef IPT_LDS_GRAD_KB
@@ -244,6 +252,10 @@ constexpr int min_blocks() {
 #ifndef IPT_ADJ_WAVE_SWEEP
 #define IPT_ADJ_WAVE_SWEEP 1
 #endif
+// Graph bins stay in LDS up to this size (KB), else global fp64 atomics.
+#ifndef IPT_GRAPH_LDS_KB
+#define IPT_GRAPH_LDS_KB 64
+#endif
 // IPT_RAY_RING=1: camera rays come from a per-wave LDS ring filled 64 at a
 // time (trace_kernel).  Brute-force adjoint only: C2 adjoint 3.01 -> 2.95 ms,
 // C3 3.93 -> 3.87 (profiles/r01_variants_ray_ring.log); the forward measured
@@ -396,7 +408,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   if (MODE == MODE_ADJ) {
     n_acc = a.grad_slots * 3;
   } else if (MODE == MODE_GRAPH && a.lds_edges) {
-    n_acc = (nT + 1) * nT * kEdgeW;
+    n_acc = (int)graph_lds_doubles(nT, nE);
   }
   // Per-triangle kd and kd/pi (the latter is BSDF's indirect `diffuse /=
   // M_PI`, path_trace.cu:15-17): computed once per workgroup with the same
@@ -705,7 +717,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         const float wf = weight * 1.f;  // Edge::update, inv_scene.h:26-36
         const double v[5] = {(double)weight, (double)wf, (double)(wf * pix.x), (double)(wf * pix.y),
                              (double)(wf * pix.z)};
-        bins_add(a.lds_edges != 0, edges, ((size_t)dst * nT + tri) * kEdgeW, 5, v);
+        const size_t bin = (size_t)dst * nT + tri;
+        bins_add(a.lds_edges != 0, edges, a.lds_edges ? bin * kEdgeL : bin * kEdgeW, 5, v);
       } else if (k == 0) {
         const TriMat &m = mat[tri];
         Le = mk(m.ke[0], m.ke[1], m.ke[2]);
@@ -821,7 +834,13 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             const double v[8] = {(double)w2, (double)wf, (double)(wf * pix.x), (double)(wf * pix.y),
                                  (double)(wf * pix.z), (double)(wf * me.ke[0]), (double)(wf * me.ke[1]),
                                  (double)(wf * me.ke[2])};
-            bins_add(a.lds_edges != 0, edges, ((size_t)tri * nT + et) * kEdgeW, 8, v);
+            const size_t bin = (size_t)tri * nT + et;
+            if (a.lds_edges) {
+              bins_add(true, edges, bin * kEdgeL, 5, v);
+              bins_add(true, edges, (size_t)(nT + 1) * nT * kEdgeL + ((size_t)tri * nE + emitter) * 3, 3, v + 5);
+            } else {
+              bins_add(false, edges, bin * kEdgeW, 8, v);
+            }
           } else {
 #ifdef IPT_ABL_DP
             const float s = ((ct * ctp) / (ts * ts)) / emit_pmf[emitter];
@@ -1121,9 +1140,18 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     __syncthreads();
     if (n_acc > 0) {
       double *dstp = (MODE == MODE_ADJ) ? grad : edges;
+      const int nb5 = (nT + 1) * nT * kEdgeL;
       for (int i = tid; i < n_acc; i += nthr) {
         const double v = lds_acc[i];
-        const int j = (MODE == MODE_ADJ && a.slot_tri) ? a.slot_tri[i / 3] * 3 + i % 3 : i;
+        int j = (MODE == MODE_ADJ && a.slot_tri) ? a.slot_tri[i / 3] * 3 + i % 3 : i;
+        if (MODE == MODE_GRAPH) {  // LDS form -> kEdgeW-wide global bins
+          if (i < nb5) {
+            j = (i / kEdgeL) * kEdgeW + i % kEdgeL;
+          } else {
+            const int q = i - nb5, dst = q / (3 * nE), ie = (q / 3) % nE;
+            j = (dst * nT + emit_tri[ie]) * kEdgeW + kEdgeL + q % 3;
+          }
+        }
         if (v != 0.0) atomicAdd(dstp + j, v);
       }
     }
@@ -1602,8 +1630,8 @@ int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const f
 int gpu_graph(GpuScene *s, const RenderParams &p, const uint8_t *target_dev, double *acc_dev, void *stream) {
   if (check_params(s, p)) return -1;
   TraceArgs a = make_args(s, p);
-  const size_t bins = (size_t)(s->host.nT + 1) * s->host.nT * kEdgeW * sizeof(double);
-  a.lds_edges = bins <= 64 * 1024 ? 1 : 0;
+  const size_t bins = graph_lds_doubles(s->host.nT, s->host.nE) * sizeof(double);
+  a.lds_edges = bins <= (size_t)IPT_GRAPH_LDS_KB * 1024 ? 1 : 0;
   a.kd_tables = 0;  // the graph integrator never reads albedo
   a.sample_major = IPT_GRAPH_SAMPLE_MAJOR;
   return launch<MODE_GRAPH>(s, a, (a.lds_edges ? bins : 0) + table_bytes(a), nullptr, nullptr, nullptr, nullptr, target_dev, acc_dev,
