@@ -661,6 +661,12 @@ template <bool SHADOW>
 __device__ __forceinline__ bool bvh_prepass(const BvhView &B, V3 p, V3 d, float &bt, int &bi, int target) {
   bt = __builtin_inff();
   bi = -1;
+#ifdef IPT_ABL_NOTARGET  // timing-only ablation build: no target test (wrong shadows)
+  if (SHADOW) {
+    bt = 1e30f;
+    bi = target;
+  } else
+#endif
   if (SHADOW) {
     hit_test(B.isect[target], target, p, d, bt, bi);
     if (bi < 0) return false;  // the target itself is missed: not the closest hit either

@@ -52,6 +52,8 @@ def scene(L, recs):
     h = C.c_void_p(0)
     assert L.ipt_load_scene(n, pos.ctypes.data_as(N.fp), ori.ctypes.data_as(N.fp), scl.ctypes.data_as(N.fp), objs,
                             mtls, C.byref(h)) > 0
+    if os.environ.get("IPT_VB_ACCEL") == "bvh":  # force the BVH instance (ablations on small scenes)
+        assert L.ipt_scene_set_accel(h, N.ACCEL_BVH) == 0
     return h
 
 
