@@ -97,7 +97,10 @@ constexpr int kLdsGradBytes = IPT_LDS_GRAD_KB * 1024;
 #define IPT_BVH_MIN_TRIS 64
 #endif
 constexpr int kBvhMinTris = IPT_BVH_MIN_TRIS;
-constexpr int kBvhLdsNodeBytes = 32 * 1024;  // stage the whole tree in LDS up to 512 nodes
+#ifndef IPT_BVH_LDS_KB
+#define IPT_BVH_LDS_KB 32
+#endif
+constexpr int kBvhLdsNodeBytes = IPT_BVH_LDS_KB * 1024;  // stage the whole tree in LDS up to 512 nodes
 
 struct TraceArgs {
   int W, H, spp, max_bounces;
