@@ -69,6 +69,7 @@ def optimize(tasks: List[SceneTask], width: int, height: int, spp: int, max_boun
             shared = torch.full((tie_shared, 3), 0.5, device="cuda", requires_grad=True)
     params = [t.kd for t in tasks] + ([shared] if shared is not None else [])
     opt = torch.optim.Adam(params, lr=lr)
+    pending = []  # (task, loss tensor) in step order
     for step in range(steps):
         opt.zero_grad(set_to_none=False)
         for i, t in enumerate(tasks):
@@ -79,7 +80,7 @@ def optimize(tasks: List[SceneTask], width: int, height: int, spp: int, max_boun
                                    seed=seed + (step * 1009 + i) * width * height * spp)
             loss = ((img - t.target) ** 2).mean()
             loss.backward()
-            t.history.append(float(loss.detach()))
+            pending.append((t, loss.detach()))  # no host sync per scene: read back once per step
         if shared is not None:
             if shared.grad is None:
                 shared.grad = torch.zeros_like(shared)
@@ -89,8 +90,19 @@ def optimize(tasks: List[SceneTask], width: int, height: int, spp: int, max_boun
             for p in params:
                 p.clamp_(0.0, 1.0)
         if log_every and step % log_every == 0 and R == 0:
+            _flush_losses(pending)
             print("step %d loss %.6g" % (step, sum(t.history[-1] for t in tasks) / max(1, len(tasks))), flush=True)
+    _flush_losses(pending)
     return shared
+
+
+def _flush_losses(pending):
+    """Move the step losses to the tasks' histories with one device->host copy."""
+    if pending:
+        vals = torch.stack([l for _, l in pending]).float().cpu().tolist()
+        for (t, _), v in zip(pending, vals):
+            t.history.append(v)
+        pending.clear()
 
 
 def main():
