@@ -4,13 +4,20 @@ box, 64 spp, 4 bounces (BASELINE.json configs[1]) on N MI355X.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-A step is one frame of the configuration: every sample of every pixel traced
-(per-sample radiance kernel + per-pixel mean kernel).  Weak scaling: each rank
-renders its own frame (disjoint sample-index ranges via frame_seed), so the
-forward has no collective; the adjoint step adds the one exchange the path has,
-an RCCL all-reduce of the per-material gradient vector.  Inputs are resident
-in HBM before the timed region; timing is HIP events on the launch stream,
-bracketed by barrier + synchronize, max over ranks.
+A step is one C2 frame, tiled across the ranks exactly as the north_star asks
+("image tiles shard across the GPUs, RCCL reduce on the per-material gradient
+vector only"): rank r traces row band r of the SAME frame (shard_rows; sample
+seeds are global indices, so the bands are the single-GPU frame's samples);
+the forward needs no collective, the adjoint step ends with ONE all-reduce of
+the nT*3 fp64 gradient.  Strong scaling: value = frame samples * K / (max
+over ranks of the time of K steps).  Inputs are resident in HBM before the
+timed region; timing is HIP events on the launch stream, bracketed by barrier
++ synchronize.
+
+Secondary lines (JSON `secondary`): weak scaling (a whole frame per rank),
+a sustained >= 0.5 s run of each leg, the per-band cost table of C2 and C4 (N =
+1: predicts the 8-GPU critical path), C3, the north_star sphere scene, C4's
+band and C5 (scene batch + Adam).
 """
 import argparse
 import ctypes as C
@@ -27,7 +34,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from inverse_path_tracer_amd import _native as N  # noqa: E402
-from inverse_path_tracer_amd.distributed import frame_seed  # noqa: E402
+from inverse_path_tracer_amd.distributed import frame_seed, shard_rows  # noqa: E402
 from inverse_path_tracer_amd.scene import ObjectSpec, Scene  # noqa: E402
 
 W = H = 512
@@ -37,14 +44,16 @@ ASSETS = os.path.join(ROOT, "assets")
 CORNELL = [ObjectSpec(os.path.join(ASSETS, "CornellBox", "CornellBox-Empty-CO.obj"),
                       os.path.join(ASSETS, "CornellBox", "CornellBox-Empty-CO.mtl"), (0, 0, 4), (0, 0, 0), (2, 2, 2))]
 # C3 (BASELINE.json configs[2]): scenes/0.txt = Cornell + the cube with its inline Kd
-SCENE0 = CORNELL + [ObjectSpec(os.path.join(ASSETS, "shapes", "cube.obj"),
-                               "*Kd 0.9041462985304743 0.5854651848798454 0.007022117649276849*", (0, -1.5, 4),
-                               (0, 0, 0), (1, 1, 1))]
+CUBE = ObjectSpec(os.path.join(ASSETS, "shapes", "cube.obj"),
+                  "*Kd 0.9041462985304743 0.5854651848798454 0.007022117649276849*", (0, -1.5, 4), (0, 0, 0),
+                  (1, 1, 1))
+SCENE0 = CORNELL + [CUBE]
 # the north_star's "+ sphere.obj" scene (not a shipped scene file): 1298 triangles, BVH
 SPHERE = CORNELL + [ObjectSpec(os.path.join(ASSETS, "shapes", "sphere.obj"), "*Kd 0.2 0.6 0.3*", (0.3, -1.2, 4.2),
                                (0.0, 0.4, 0.0), (1.2, 1.2, 1.2))]
 # casts/sample counted by the CPU oracle over the full C2
-# frame (tools/count_casts.py -> profiles/casts_per_sample.json)
+# frame (tools/count_casts.py -> profiles/casts_per_sample.json; re-derived
+# by tests/test_gpu_full.py::test_c2_forward_full_frame_bit_exact)
 CASTS_PER_SAMPLE = 5.694442272186279
 N_TRIANGLES = 18
 FLOP_PER_TEST = 38          # F1 test with hoisted edge planes
@@ -55,59 +64,172 @@ PMC_FILE = os.path.join(ROOT, "profiles", "pmc_fwd_trace_kernel.json")
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
-                    help="skip the C3/C4/BVH-scene lines (profiling runs: keeps the C2 kernel's statistics pure)")
+                    help="skip the secondary lines (profiling runs: keeps the C2 kernel's statistics pure)")
     return ap.parse_args()
 
 
-def cpu_baseline(fwd_seconds=8.0, one_core_seconds=3.0, adj_seconds=4.0):
-    """The CPU oracle (test infrastructure, oracle/ipt_oracle.c -O2 OpenMP) on
-    bounded samples of the same C2 workload: whole frames (consecutive frame
-    seeds) on this rank's allowed cores (capped at 16) until fwd_seconds, the
-    first rows on ONE core, and the adjoint on the first rows."""
+# ----------------------------------------------------------------- CPU baseline
+def cpu_baseline(seconds_per_leg=1.5):
+    """The CPU oracle (test infrastructure, oracle/ipt_oracle.c) on bounded
+    samples of C1, C2 and the C3 adjoint: rows of the frame until each leg has
+    run `seconds_per_leg`, with the parity build (-O2 -ffp-contract=off) and
+    the fast build (-O3 x86-64-v3, FMA contraction), on this rank's share of
+    the host cores and on one core."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
 
-    cores = min(16, len(os.sched_getaffinity(0)))
-    L = oracle_lib.lib()
-    recs = [(o.pos, o.ori, o.scl, o.obj_file, o.mtl_file) for o in CORNELL]
-    sc = oracle_lib.OracleScene(recs)
+    affinity = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS") or affinity)
+    cores = max(1, min(share, affinity))
+    recs = {"cornell": [(o.pos, o.ori, o.scl, o.obj_file, o.mtl_file) for o in CORNELL],
+            "scene0": [(o.pos, o.ori, o.scl, o.obj_file, o.mtl_file) for o in SCENE0]}
+    legs = {"c1_fwd": ("cornell", 128, 128, 8, 2, "fwd"), "c2_fwd": ("cornell", W, H, SPP, BOUNCES, "fwd"),
+            "c3_adj": ("scene0", W, H, SPP, BOUNCES, "adj")}
+    out = {}
+    for fast in (False, True):
+        scenes = {k: oracle_lib.OracleScene(v, fast=fast) for k, v in recs.items()}
+        L = oracle_lib.lib(fast)
+        for threads in (cores, 1):
+            L.oro_set_threads(threads)
+            for leg, (sc_name, w, h, spp, mb, kind) in legs.items():
+                sc = scenes[sc_name]
+                adj = np.ones((h, w, 3), np.float32)
+                rows, row, total, secs = 2, 0, 0, 0.0
+                while secs < seconds_per_leg and total < 64 * h:  # rows in frame order, wrapping (C1 is small)
+                    r = min(rows, h - row)
+                    t0 = time.perf_counter()
+                    if kind == "fwd":
+                        sc.render_samples(w, h, spp, mb, 0, row * w * spp, (row + r) * w * spp)
+                    else:
+                        sc.adjoint(w, h, spp, mb, 0, adj, row, row + r)
+                    secs += time.perf_counter() - t0
+                    total += r
+                    row = (row + r) % h
+                    rows *= 2
+                key = "%s_%s_%s" % (leg, "fast" if fast else "parity", "1core" if threads == 1 else "all")
+                out[key] = {"Msamples_s": round(total * w * spp / secs / 1e6, 3), "rows": total, "s": round(secs, 2)}
+        L.oro_set_threads(cores)
+    c2 = out["c2_fwd_fast_all"]
+    return {"value": c2["Msamples_s"], "unit": "Msamples/s", "cores": cores, "kind": "port",
+            "sample": "CPU oracle (oracle/ipt_oracle.c) fast build (-O3 x86-64-v3 -fopenmp) on %d rows of the "
+                      "C2 frame (%.1f s); legs: C1/C2 forward and C3 adjoint, parity and fast builds, %d cores and "
+                      "1 core, >= %.1f s each (table in `legs`)" % (c2["rows"], c2["s"], cores, seconds_per_leg),
+            "grad_value": out["c3_adj_fast_all"]["Msamples_s"], "value_1core": out["c2_fwd_fast_1core"]["Msamples_s"],
+            "cores_note": "%d = this job's CPU share (OMP_NUM_THREADS on the GPU box; %d CPUs in the affinity mask, "
+                          "%d in the machine)" % (cores, affinity, os.cpu_count() or 0),
+            "legs": out}
 
-    def rows_for(seconds, fn):
-        rows, done, secs = 4, 0, 0.0
-        while secs < seconds and done < H:
-            r = min(rows, H - done)
-            t0 = time.perf_counter()
-            fn(done, done + r)
-            secs += time.perf_counter() - t0
-            done += r
-            rows *= 2
-        return done, secs
 
-    L.oro_set_threads(cores)
-    frames, secs = 0, 0.0
-    while secs < fwd_seconds and frames < 16:
-        t0 = time.perf_counter()
-        sc.render_samples(W, H, SPP, BOUNCES, frame_seed(0, frames, W, H, SPP))
-        secs += time.perf_counter() - t0
-        frames += 1
-    fwd = frames * W * H * SPP / secs / 1e6
-    adj = np.ones((H, W, 3), np.float32)
-    arows, asecs = rows_for(adj_seconds, lambda b, e: sc.adjoint(W, H, SPP, BOUNCES, 0, adj, b, e))
-    L.oro_set_threads(1)
-    orows, osecs = rows_for(one_core_seconds,
-                            lambda b, e: sc.render_samples(W, H, SPP, BOUNCES, 0, b * W * SPP, e * W * SPP))
-    L.oro_set_threads(cores)
-    return {"value": round(fwd, 3), "unit": "Msamples/s", "cores": cores, "kind": "port",
-            "sample": "CPU oracle (oracle/ipt_oracle.c, -O2 OpenMP) on %d whole C2 frame(s) (%d samples, %.1f s); "
-                      "adjoint on rows [0,%d) (%.1f s); 1 core on rows [0,%d) (%.1f s)" % (
-                          frames, frames * W * H * SPP, secs, arows, asecs, orows, osecs),
-            "grad_value": round(arows * W * SPP / asecs / 1e6, 3),
-            "value_1core": round(orows * W * SPP / osecs / 1e6, 3)}
+# ----------------------------------------------------------------- GPU timing helpers
+class Ctx:
+    def __init__(self, dev, world, rank):
+        self.dev, self.world, self.rank = dev, world, rank
+        self.stream = torch.cuda.current_stream(dev)
+        self.st = self.stream.cuda_stream
+        self.L = N.lib()
+
+    def barrier(self):
+        torch.cuda.synchronize(self.dev)
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(self.dev)
+
+    def max_over_ranks(self, x):
+        if self.world == 1:
+            return x
+        t = torch.tensor([x], device=self.dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def timed(self, fn, k):
+        """ms for k calls of fn(i) on the stream (barrier-bracketed, max over ranks)."""
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        self.barrier()
+        e0.record(self.stream)
+        for i in range(k):
+            fn(i)
+        e1.record(self.stream)
+        self.barrier()
+        return self.max_over_ranks(e0.elapsed_time(e1))
+
+    def sustained(self, fn, seconds=0.5):
+        """Back-to-back calls until >= `seconds` of GPU time: (calls, ms)."""
+        k, ms = 4, 0.0
+        while True:
+            ms = self.timed(fn, k)
+            if ms >= seconds * 1e3 or k >= 1 << 16:
+                return k, ms
+            k = max(k * 2, int(k * seconds * 1e3 / max(ms, 1e-3) * 1.1) + 1)
+
+
+class Leg:
+    """One workload on one scene: forward (sample-major buffer + pixel mean)
+    and adjoint (+ gradient all-reduce) over rows [b, e)."""
+
+    def __init__(self, cx, objs, w, h, spp, mb, b=0, e=None, seed=0):
+        self.cx, self.w, self.h, self.spp, self.mb, self.seed = cx, w, h, spp, mb, seed
+        self.b, self.e = b, (h if e is None else e)
+        self.sc = Scene(objs)
+        dev = cx.dev
+        npix = (self.e - self.b) * w
+        self.npix = npix
+        self.samples = torch.empty((npix * spp, 3), device=dev, dtype=torch.float32)
+        self.hdr = torch.empty((npix, 3), device=dev, dtype=torch.float32)
+        self.adj = torch.full((h, w, 3), 1.0 / (3 * w * h), device=dev, dtype=torch.float32)
+        self.grad = torch.zeros((self.sc.nT, 3), device=dev, dtype=torch.float64)
+        self.kev = []
+
+    def params(self, step):
+        return N.make_params(self.w, self.h, self.spp, self.mb, frame_seed(self.seed, step, self.w, self.h, self.spp),
+                             self.b, self.e)
+
+    def fwd(self, step, ev=None):
+        cx, p = self.cx, self.params(step)
+        if ev is not None:
+            ev[0].record(cx.stream)
+        N.check(cx.L.ipt_render_samples_sm_dev(self.sc.handle, C.byref(p), None, self.samples.data_ptr(), cx.st))
+        if ev is not None:
+            ev[1].record(cx.stream)
+        N.check(cx.L.ipt_pixel_mean_sm_dev(self.samples.data_ptr(), self.npix, self.spp, self.hdr.data_ptr(), None,
+                                           cx.st))
+
+    def adjoint(self, step, reduce=True):
+        cx, p = self.cx, self.params(step)
+        self.grad.zero_()
+        N.check(cx.L.ipt_adjoint_dev(self.sc.handle, C.byref(p), None, self.adj.data_ptr(), self.grad.data_ptr(),
+                                     cx.st))
+        if reduce and cx.world > 1:
+            dist.all_reduce(self.grad)  # the per-material gradient vector, nT*3 fp64 (720 B for 30 triangles)
+
+    def samples_per_call(self):
+        return (self.e - self.b) * self.w * self.spp
+
+    def close(self):
+        self.sc.close()
+
+
+def band_table(cx, objs, w, h, spp, mb, n=8, reps=2):
+    """Each of the n row bands of one frame timed alone (forward, adjoint): the
+    critical path of an n-GPU tile split is the slowest band."""
+    rows = []
+    for r in range(n):
+        b, e = shard_rows(h, n, r)
+        leg = Leg(cx, objs, w, h, spp, mb, b, e)
+        leg.fwd(10**6)
+        leg.adjoint(10**6, reduce=False)
+        f = cx.timed(lambda i: leg.fwd(i), reps) / reps
+        a = cx.timed(lambda i: leg.adjoint(i, reduce=False), reps) / reps
+        rows.append({"rows": [b, e], "fwd_ms": round(f, 4), "adj_ms": round(a, 4)})
+        leg.close()
+    fw = [x["fwd_ms"] for x in rows]
+    ad = [x["adj_ms"] for x in rows]
+    return {"bands": rows, "fwd_max_over_mean": round(max(fw) / np.mean(fw), 4),
+            "adj_max_over_mean": round(max(ad) / np.mean(ad), 4)}
 
 
 def main():
@@ -119,160 +241,79 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
-    scene = Scene(CORNELL)
-    stream = torch.cuda.current_stream(dev)
-    st = stream.cuda_stream
-    L = N.lib()
-    npix = W * H
-    samples = torch.empty((npix * SPP, 3), device=dev, dtype=torch.float32)
-    hdr = torch.empty((H, W, 3), device=dev, dtype=torch.float32)
-    adj = torch.full((H, W, 3), 1.0 / (3 * npix), device=dev, dtype=torch.float32)
-    grad = torch.zeros((scene.nT, 3), device=dev, dtype=torch.float64)
-
-    def params(step):
-        return N.make_params(W, H, SPP, BOUNCES, frame_seed(args.seed, rank * 100003 + step, W, H, SPP))
-
-    def fwd(step, ev=None):
-        p = params(step)
-        if ev is not None:
-            ev[0].record(stream)
-        N.check(L.ipt_render_samples_sm_dev(scene.handle, C.byref(p), None, samples.data_ptr(), st))
-        if ev is not None:
-            ev[1].record(stream)
-        N.check(L.ipt_pixel_mean_sm_dev(samples.data_ptr(), npix, SPP, hdr.data_ptr(), None, st))
-
-    def bwd(step):
-        p = params(step)
-        grad.zero_()
-        N.check(L.ipt_adjoint_dev(scene.handle, C.byref(p), None, adj.data_ptr(), grad.data_ptr(), st))
-        if world > 1:
-            dist.all_reduce(grad)  # the per-material gradient vector, nT*3 fp64
-
-    def barrier():
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-
-    def max_over_ranks(x):
-        if world == 1:
-            return x
-        t = torch.tensor([x], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
-
+    cx = Ctx(dev, world, rank)
+    b, e = shard_rows(H, world, rank)
+    head = Leg(cx, CORNELL, W, H, SPP, BOUNCES, b, e, seed=args.seed)
     for i in range(args.warmup):
-        fwd(10**6 + i)
-        bwd(10**6 + i)
-    # ---------------------------------------------------------------- forward
+        head.fwd(10**6 + i)
+        head.adjoint(10**6 + i)
+    # ---------------------------------------------------------- headline: tile-split C2 frame
     kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    barrier()
     t_wall = time.perf_counter()
-    e0.record(stream)
-    for i in range(args.steps):
-        fwd(i, kev[i])
-    e1.record(stream)
-    barrier()
+    fwd_ms = cx.timed(lambda i: head.fwd(i, kev[i]), args.steps)
     wall_fwd = time.perf_counter() - t_wall
-    fwd_ms = max_over_ranks(e0.elapsed_time(e1))
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in kev]))
-    # ---------------------------------------------------------------- adjoint
-    barrier()
-    e0.record(stream)
-    for i in range(args.steps):
-        bwd(i)
-    e1.record(stream)
-    barrier()
-    bwd_ms = max_over_ranks(e0.elapsed_time(e1))
-    # ------------------------------------------- secondary workloads (info)
+    kernel_ms = float(np.mean([a.elapsed_time(z) for a, z in kev]))
+    bwd_ms = cx.timed(lambda i: head.adjoint(i), args.steps)
+    frame = W * H * SPP
+    value = args.steps * frame / (fwd_ms / 1e3) / 1e6
+    grad_value = args.steps * frame / (bwd_ms / 1e3) / 1e6
+
     extra = {}
-    for key, objs, kind in (() if args.no_secondary else (("c3_grad", SCENE0, "adj"), ("bvh_fwd", SPHERE, "fwd"))):
-        sc = Scene(objs)
-        g2 = torch.zeros((sc.nT, 3), device=dev, dtype=torch.float64)
-
-        def run(step):
-            p = params(step)
-            if kind == "adj":
-                g2.zero_()
-                N.check(L.ipt_adjoint_dev(sc.handle, C.byref(p), None, adj.data_ptr(), g2.data_ptr(), st))
-                if world > 1:
-                    dist.all_reduce(g2)
-            else:
-                N.check(L.ipt_render_samples_sm_dev(sc.handle, C.byref(p), None, samples.data_ptr(), st))
-
-        k = max(1, min(args.steps, 5))
-        run(10**6)
-        barrier()
-        e0.record(stream)
-        for i in range(k):
-            run(i)
-        e1.record(stream)
-        barrier()
-        ms = max_over_ranks(e0.elapsed_time(e1)) / k
-        extra[key] = {"value": round(world * W * H * SPP / ms / 1e3, 2),
-                      "unit": "grad-Msamples/s" if kind == "adj" else "Msamples/s", "ms_per_step": round(ms, 4),
-                      "triangles": sc.nT, "accel": sc.bvh_info()["accel"],
-                      "workload": ("C3: scenes/0.txt (Cornell + cube), 512x512, 64 spp, 4 bounces, adjoint dL/dKd "
-                                   "+ all-reduce" if kind == "adj" else
-                                   "Cornell + sphere.obj (north_star scene), 512x512, 64 spp, 4 bounces, forward")}
-        sc.close()
-    # C4 (BASELINE.json configs[3]): scenes/0.txt, 1024x1024, 256 spp, 8 bounces,
-    # rank k traces row band k of 8 (the 8-GPU sharding); forward + adjoint
-    # with the one gradient all-reduce.  At N < 8 only bands 0..N-1 run.
-    if world <= 8 and not args.no_secondary:
-        from inverse_path_tracer_amd.distributed import shard_rows
-        W4, S4, B4 = 1024, 256, 8
-        b4, e4 = shard_rows(W4, 8, rank)
-        sc = Scene(SCENE0)
-        g4 = torch.zeros((sc.nT, 3), device=dev, dtype=torch.float64)
-        adj4 = torch.full((W4, W4, 3), 1.0 / (3 * W4 * W4), device=dev, dtype=torch.float32)
-        smp4 = torch.empty(((e4 - b4) * W4 * S4, 3), device=dev, dtype=torch.float32)
-        p4 = N.make_params(W4, W4, S4, B4, args.seed, b4, e4)
-        res4 = {}
-        for kind in ("fwd", "adj"):
-            def run4():
-                if kind == "fwd":
-                    N.check(L.ipt_render_samples_sm_dev(sc.handle, C.byref(p4), None, smp4.data_ptr(), st))
-                else:
-                    g4.zero_()
-                    N.check(L.ipt_adjoint_dev(sc.handle, C.byref(p4), None, adj4.data_ptr(), g4.data_ptr(), st))
-                    if world > 1:
-                        dist.all_reduce(g4)
-            run4()
-            barrier()
-            e0.record(stream)
-            for _ in range(2):
-                run4()
-            e1.record(stream)
-            barrier()
-            res4[kind] = max_over_ranks(e0.elapsed_time(e1)) / 2
-        n4 = world * (e4 - b4) * W4 * S4
-        extra["c4"] = {"value": round(n4 / res4["fwd"] / 1e3, 2), "unit": "Msamples/s",
-                       "grad_value": round(n4 / res4["adj"] / 1e3, 2), "grad_unit": "grad-Msamples/s",
-                       "fwd_ms": round(res4["fwd"], 3), "adj_ms": round(res4["adj"], 3), "bands": "%d of 8" % world,
-                       "workload": "C4: scenes/0.txt, 1024x1024, 256 spp, 8 bounces; rank k = row band k of 8 "
-                                   "(forward, adjoint + all-reduce)"}
-        sc.close()
-        del smp4
-
-    samples_per_frame = W * H * SPP
-    value = world * args.steps * samples_per_frame / (fwd_ms / 1e3) / 1e6
-    grad_value = world * args.steps * samples_per_frame / (bwd_ms / 1e3) / 1e6
-    # roofline of the dominant kernel (trace_kernel<FWD>), SURVEY.md §8(d)
-    flop_per_launch = samples_per_frame * CASTS_PER_SAMPLE * N_TRIANGLES * FLOP_PER_TEST
+    if not args.no_secondary:
+        # sustained rates (>= 0.5 s of back-to-back steps per leg; DVFS-steady)
+        k, ms = cx.sustained(lambda i: head.fwd(i))
+        ka, msa = cx.sustained(lambda i: head.adjoint(i))
+        extra["sustained"] = {"fwd_Msamples_s": round(k * frame / ms / 1e3, 2), "fwd_steps": k, "fwd_s": round(ms / 1e3, 3),
+                              "grad_Msamples_s": round(ka * frame / msa / 1e3, 2), "adj_steps": ka,
+                              "adj_s": round(msa / 1e3, 3)}
+        # weak scaling: every rank traces a whole frame of its own
+        weak = Leg(cx, CORNELL, W, H, SPP, BOUNCES, seed=args.seed + (rank + 1) * 7919 * frame)
+        kw = max(4, min(args.steps, 40))
+        wf = cx.timed(lambda i: weak.fwd(i), kw)
+        wa = cx.timed(lambda i: weak.adjoint(i), kw)
+        extra["weak"] = {"value": round(world * kw * frame / wf / 1e3, 2), "grad_value": round(world * kw * frame / wa / 1e3, 2),
+                         "unit": "Msamples/s", "workload": "C2, one whole frame per rank per step (frame-parallel)"}
+        weak.close()
+        # other configurations, this rank's band of an N-way tile split
+        for key, objs, w, h, spp, mb, desc in (
+                ("c3", SCENE0, W, H, SPP, BOUNCES, "C3: scenes/0.txt (Cornell + cube, 30 triangles), 512x512, 64 spp, 4 bounces"),
+                ("bvh_sphere", SPHERE, W, H, SPP, BOUNCES, "Cornell + sphere.obj (1298 triangles, BVH), 512x512, 64 spp, 4 bounces"),
+                ("c4", SCENE0, 1024, 1024, 256, 8, "C4: scenes/0.txt, 1024x1024, 256 spp, 8 bounces")):
+            bb, ee = shard_rows(h, world, rank) if key != "c4" else shard_rows(h, 8, rank) if world <= 8 else (0, 0)
+            leg = Leg(cx, objs, w, h, spp, mb, bb, ee)
+            leg.fwd(10**6)
+            leg.adjoint(10**6)
+            reps = 2 if key == "c4" else 5
+            f = cx.timed(lambda i: leg.fwd(i), reps) / reps
+            a = cx.timed(lambda i: leg.adjoint(i), reps) / reps
+            n = leg.samples_per_call() * world
+            extra[key] = {"value": round(n / f / 1e3, 2), "unit": "Msamples/s", "grad_value": round(n / a / 1e3, 2),
+                          "grad_unit": "grad-Msamples/s", "fwd_ms": round(f, 4), "adj_ms": round(a, 4),
+                          "triangles": leg.sc.nT, "accel": leg.sc.bvh_info()["accel"],
+                          "workload": desc + ("; rank k = row band k of 8 (%d of 8 bands run)" % min(world, 8)
+                                              if key == "c4" else "; tile split over %d rank(s)" % world)}
+            leg.close()
+        if world == 1:
+            extra["bands_c2"] = band_table(cx, CORNELL, W, H, SPP, BOUNCES, reps=4)
+            extra["bands_c4"] = band_table(cx, SCENE0, 1024, 1024, 256, 8, reps=1)
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            import bench_c5
+            extra["c5"] = bench_c5.run(scenes=13, steps=20, warmup=3, total=23)
+    # ---------------------------------------------------------- roofline of the dominant kernel
+    band_samples = head.samples_per_call()
+    flop_per_launch = band_samples * CASTS_PER_SAMPLE * N_TRIANGLES * FLOP_PER_TEST
     achieved = flop_per_launch / (kernel_ms / 1e3) / 1e12
     traffic = None
     if os.path.exists(PMC_FILE):
         with open(PMC_FILE) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
-    # SURVEY.md §8(d) "HBM fraction": PMC-measured bytes of the same kernel
-    # (profiles/, FETCH x2 + WRITE) over this run's kernel time, vs 8 TB/s
+        if world > 1 and traffic:
+            traffic = traffic * band_samples / frame  # the counters were taken on the whole frame
     hbm = None
     if traffic:
         gbs = traffic / (kernel_ms / 1e3) / 1e9
         hbm = {"bytes_per_launch": traffic, "achieved_GBps": round(gbs, 1), "peak_GBps": 8000.0,
-               "frac": round(gbs / 8000.0, 4), "algorithmic_bytes_per_launch": samples_per_frame * 12,
+               "frac": round(gbs / 8000.0, 4), "algorithmic_bytes_per_launch": band_samples * 12,
                "source": os.path.relpath(PMC_FILE, ROOT)}
     roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
@@ -288,17 +329,19 @@ def main():
             "metric": "Msamples/sec fwd + grad-Msamples/sec, 512² Cornell 64spp, 1/2/4/8 GPU",
             "value": round(value, 2), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(fwd_ms / args.steps, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": "C2: CornellBox-Empty-CO.obj, 512x512, 64 spp, max_bounces=4, one frame per "
-                                   "rank per step (fwd); adjoint dL/dKd per frame + RCCL all-reduce (grad)",
-                       "width": W, "height": H, "spp": SPP, "max_bounces": BOUNCES, "triangles": scene.nT,
-                       "parallelism": "frame-parallel x%d" % world},
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "C2: CornellBox-Empty-CO.obj, 512x512, 64 spp, max_bounces=4; one frame per step "
+                                   "tiled over the ranks as row bands (fwd); adjoint dL/dKd of the band + RCCL "
+                                   "all-reduce of the gradient (grad)",
+                       "width": W, "height": H, "spp": SPP, "max_bounces": BOUNCES, "triangles": head.sc.nT,
+                       "parallelism": "row-band tiles x%d" % world, "rank0_rows": [b, e]},
             "grad_value": round(grad_value, 2), "grad_unit": "grad-Msamples/s",
             "grad_ms_per_step": round(bwd_ms / args.steps, 4),
             "wall_s_fwd_region": round(wall_fwd, 4),
             "roofline": roofline, "hbm": hbm, "cpu_baseline": cpu, "secondary": extra,
         }
         print(json.dumps(out), flush=True)
+    head.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

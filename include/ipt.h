@@ -158,6 +158,20 @@ int ipt_adjoint_dev(void *scene, const ipt_params_t *p, const float *kd_dev, con
                     void *stream);
 int ipt_graph_dev(void *scene, const ipt_params_t *p, const uint8_t *target_dev, double *acc_dev, void *stream);
 
+/* Scene batch (BASELINE config C5 over scenes/0..99.txt, which share their
+ * geometry and differ only in the cube's Kd; the reference renders them one
+ * loadScene/createImage at a time, ipt_cuda.py:115-134): n_scenes material
+ * sets over ONE loaded geometry in one launch.  Set b uses kd_dev + b*nT*3
+ * and seed p->seed + b*seed_stride, and equals ipt_render_dev /
+ * ipt_adjoint_dev of that kd and seed (images bit for bit, gradients to fp64
+ * summation order).  hdr_dev: n_scenes*rows*W*3; adj_dev: n_scenes*H*W*3
+ * (full frames, indexed by global pixel like ipt_adjoint_dev); grad_dev:
+ * n_scenes*nT*3, accumulated. */
+int ipt_render_batch_dev(void *scene, const ipt_params_t *p, int n_scenes, uint64_t seed_stride, const float *kd_dev,
+                         float *hdr_dev, void *stream);
+int ipt_adjoint_batch_dev(void *scene, const ipt_params_t *p, int n_scenes, uint64_t seed_stride, const float *kd_dev,
+                          const float *adj_dev, double *grad_dev, void *stream);
+
 /* PNG helpers (RGB8). ipt_png_read with rgb == NULL only reports the size. */
 int ipt_png_write(const char *path, int width, int height, const uint8_t *rgb);
 int ipt_png_read(const char *path, int *width, int *height, uint8_t *rgb, int64_t capacity);

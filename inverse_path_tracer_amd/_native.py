@@ -90,6 +90,8 @@ SIGNATURES = {
     "ipt_pixel_mean_sm_dev": (C.c_int, [vp, C.c_int64, C.c_int, vp, vp, vp]),
     "ipt_adjoint_dev": (C.c_int, [vp, pp, vp, vp, vp, vp]),
     "ipt_graph_dev": (C.c_int, [vp, pp, vp, vp, vp]),
+    "ipt_render_batch_dev": (C.c_int, [vp, pp, C.c_int, C.c_uint64, vp, vp, vp]),
+    "ipt_adjoint_batch_dev": (C.c_int, [vp, pp, C.c_int, C.c_uint64, vp, vp, vp, vp]),
     "ipt_scene_set_accel": (C.c_int, [vp, C.c_int]),
     "ipt_scene_bvh_info": (C.c_int, [vp, C.POINTER(C.c_int32)]),
     "ipt_scene_export_bvh": (C.c_int, [vp, fp, fp, C.POINTER(C.c_int32)]),

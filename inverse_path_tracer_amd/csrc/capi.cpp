@@ -375,6 +375,32 @@ int ipt_adjoint_dev(void *scene, const ipt_params_t *p, const float *kd_dev, con
   return gpu_status(ipt::gpu_adjoint(s, to_params(p), kd_dev, adj_dev, grad_dev, stream));
 }
 
+int ipt_render_batch_dev(void *scene, const ipt_params_t *p, int n_scenes, uint64_t seed_stride, const float *kd_dev,
+                         float *hdr_dev, void *stream) {
+  GpuScene *s = as_scene(scene);
+  if (!s || !p || !kd_dev || !hdr_dev || n_scenes < 1) {
+    if (s) fail("ipt_render_batch_dev: bad arguments (kd_dev and hdr_dev are required, n_scenes >= 1)");
+    return -1;
+  }
+  ipt::RenderParams r = to_params(p);
+  r.nscenes = n_scenes;
+  r.seed_stride = seed_stride;
+  return gpu_status(ipt::gpu_render(s, r, kd_dev, hdr_dev, nullptr, stream));
+}
+
+int ipt_adjoint_batch_dev(void *scene, const ipt_params_t *p, int n_scenes, uint64_t seed_stride, const float *kd_dev,
+                          const float *adj_dev, double *grad_dev, void *stream) {
+  GpuScene *s = as_scene(scene);
+  if (!s || !p || !kd_dev || !adj_dev || !grad_dev || n_scenes < 1) {
+    if (s) fail("ipt_adjoint_batch_dev: bad arguments (kd_dev, adj_dev and grad_dev are required, n_scenes >= 1)");
+    return -1;
+  }
+  ipt::RenderParams r = to_params(p);
+  r.nscenes = n_scenes;
+  r.seed_stride = seed_stride;
+  return gpu_status(ipt::gpu_adjoint(s, r, kd_dev, adj_dev, grad_dev, stream));
+}
+
 int ipt_graph_dev(void *scene, const ipt_params_t *p, const uint8_t *target_dev, double *acc_dev, void *stream) {
   GpuScene *s = as_scene(scene);
   if (!s || !p || !target_dev || !acc_dev) return -1;

@@ -143,6 +143,13 @@ struct TraceArgs {
   // float x: both are the correctly rounded x * 2^-k), else 0
   float rc_spp;
   int use_ring;  // RING instances: camera rays from the LDS ring (host decides: only if it costs no residency)
+  // scene batch (C5): blocks [b * bps, (b+1) * bps) trace material set b --
+  // kd + b*3nT, seed + b*seed_stride, outputs at b * (out|adj)_stride,
+  // gradient at b*3nT -- so each workgroup holds ONE set's tables and bins
+  // (the single-scene LDS footprint) and every set is the single-scene
+  // launch of its own kd and seed
+  int nscenes, bps;
+  uint64_t seed_stride, out_stride, adj_stride;
 };
 
 __device__ __forceinline__ uint32_t udiv32(uint32_t n, uint64_t m, uint32_t d) {
@@ -168,7 +175,8 @@ using namespace dev;
 // Work item w of a launch -> global sample g, pixel (r, c), XORWOW state
 // after the two camera draws and the camera ray (path_trace.cu:150-165); the
 // enumeration is described in trace_kernel.
-__device__ __forceinline__ void item_ray(const TraceArgs &a, uint64_t w, Rng &st, V3 &p, V3 &d, int &r, int &c) {
+__device__ __forceinline__ void item_ray(const TraceArgs &a, uint64_t seed, uint64_t w, Rng &st, V3 &p, V3 &d, int &r,
+                                         int &c) {
   uint64_t g;
   if (a.idx32) {
     uint32_t pixel;
@@ -195,7 +203,7 @@ __device__ __forceinline__ void item_ray(const TraceArgs &a, uint64_t w, Rng &st
     r = (int)(pixel / (uint64_t)a.W);
     c = (int)(pixel % (uint64_t)a.W);
   }
-  rng_init(st, a.seed + g);
+  rng_init(st, seed + g);
   camera_ray(a.cam, st, r, c, a.W, a.H, p, d);
 }
 
@@ -401,6 +409,20 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     double *__restrict__ edges) {
   extern __shared__ double lds[];
   const int tid = threadIdx.x;
+  // scene batch: this workgroup's material set and its place among the set's blocks
+  const int set = a.nscenes > 1 ? (int)(blockIdx.x / (uint32_t)a.bps) : 0;
+  const uint32_t sblock = blockIdx.x - (uint32_t)set * (uint32_t)(a.nscenes > 1 ? a.bps : 0);
+  const uint32_t sgrid = a.nscenes > 1 ? (uint32_t)a.bps : gridDim.x;
+  const uint64_t seed = a.seed + (uint64_t)set * a.seed_stride;
+  if (a.nscenes > 1) {
+    kd += (size_t)set * 3 * a.nT;
+    if (MODE == MODE_FWD) out_samples += (size_t)set * a.out_stride;
+    if (MODE == MODE_ADJ) {
+      adj += (size_t)set * a.adj_stride;
+      grad += (size_t)set * 3 * a.nT;
+    }
+  }
+  const float *kdpi_g = a.kdpi_g ? a.kdpi_g + (size_t)set * 3 * a.nT : nullptr;
   constexpr bool SERVE = BVH && IPT_BVH_SERVER;  // + a traversal-server wave
   constexpr int nthr = block_threads<BVH>();
   const int nT = a.nT, nE = a.nE;
@@ -436,7 +458,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   };
   auto kdpi3 = [&](int t) -> V3 {
     if (a.kd_tables) return mk(tab_l[3 * nT + 3 * t], tab_l[3 * nT + 3 * t + 1], tab_l[3 * nT + 3 * t + 2]);
-    const gbl_f32 *q = (const gbl_f32 *)a.kdpi_g + 3 * t;
+    const gbl_f32 *q = (const gbl_f32 *)kdpi_g + 3 * t;
     return mk(q[0], q[1], q[2]);
   };
   // edge-plane offsets of each triangle pair for the unrolled small-scene
@@ -537,8 +559,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
 
   if (!SERVE || tid < kBlock) {  // path waves
   // wave-uniform sample range (static partition, regenerated per lane)
-  const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * kBlock + tid) >> 6);
-  const uint32_t nwaves = (gridDim.x * kBlock) >> 6;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((sblock * kBlock + tid) >> 6);
+  const uint32_t nwaves = (sgrid * kBlock) >> 6;
   // Work items w in [0, n_samples) of this launch.  Pixel-major: w is sample
   // g = s_begin + w (a wave traces consecutive samples of one pixel).
   // Sample-major (FWD into a [s][pixel][3] buffer): w = s * npix + pixel, so
@@ -589,7 +611,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             Rng s2;
             V3 p2, d2;
             int r2, c2;
-            item_ray(a, w, s2, p2, d2, r2, c2);
+            item_ray(a, seed, w, s2, p2, d2, r2, c2);
             float *q = ring + lane;
             q[0] = d2.x; q[64] = d2.y; q[128] = d2.z;
             q[192] = __uint_as_float(s2.d); q[256] = __uint_as_float(s2.v0); q[320] = __uint_as_float(s2.v1);
@@ -640,7 +662,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         if (w < end) {
           witem = w;
           int r, c;
-          item_ray(a, w, st, p, d, r, c);
+          item_ray(a, seed, w, st, p, d, r, c);
           L = mk(0.f, 0.f, 0.f);
           Le = L;
           Ld = L;
@@ -1169,6 +1191,10 @@ __global__ __launch_bounds__(kBlock) void pixel_mean_sm_kernel(const float *__re
                                                                uint8_t *__restrict__ ldr) {
   const int64_t px = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (px >= npix) return;
+  // scene batch: blockIdx.y = material set, each with its own [s][pixel][3] buffer and image
+  samples += (size_t)blockIdx.y * (size_t)npix * spp * 3;
+  hdr += (size_t)blockIdx.y * (size_t)npix * 3;
+  if (ldr) ldr += (size_t)blockIdx.y * (size_t)npix * 3;
   float tx = 0.f, ty = 0.f, tz = 0.f;
   const float fs = (float)spp;
   for (int i = 0; i < spp; ++i) {
@@ -1223,9 +1249,6 @@ struct GpuScene {
   float *kd = nullptr;
   int *emit_tri = nullptr;
   float *emit_cdf = nullptr, *emit_pmf = nullptr;
-  float *ws = nullptr;  // per-sample radiance workspace
-  size_t ws_bytes = 0;
-  float *kdpi = nullptr;  // kd / pi of the launch's albedo, when kd does not fit LDS tables
   bool has_ks = false;      // some material has a Phong lobe
   BvhNode *bnodes = nullptr;
   BvhPair *bpairs = nullptr;
@@ -1286,6 +1309,13 @@ GpuScene *gpu_upload(const HostScene &host, std::string *err) {
     return nullptr;
   }
   for (const TriMat &m : host.mat) s->has_ks |= (m.flags & MAT_HAS_KS) != 0;
+  {  // keep stream-ordered scratch blocks in the pool between launches
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, s->device) == hipSuccess) {
+      uint64_t keep = ~0ull;
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
+  }
   if ((size_t)host.nT * 3 * sizeof(double) > (size_t)kLdsGradBytes) {
     // adjoint gradient bins: the largest triangles (most path vertices land on
     // them, so their bins are the contended ones) get LDS slots
@@ -1329,8 +1359,6 @@ void gpu_free(GpuScene *s) {
   (void)hipFree(s->emit_tri);
   (void)hipFree(s->emit_cdf);
   (void)hipFree(s->emit_pmf);
-  (void)hipFree(s->ws);
-  (void)hipFree(s->kdpi);
   (void)hipFree(s->bnodes);
   (void)hipFree(s->bpairs);
   (void)hipFree(s->big_pairs);
@@ -1371,6 +1399,10 @@ static int check_params(const GpuScene *s, const RenderParams &p) {
   }
   if (s->host.nT <= 0) {
     gpu_set_error("scene has no triangles");
+    return -1;
+  }
+  if (p.nscenes < 1) {
+    gpu_set_error("scene batch needs n_scenes >= 1");
     return -1;
   }
   return 0;
@@ -1446,6 +1478,11 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.slot_tri = nullptr;
   std::memcpy(a.cam, s->host.cam, sizeof a.cam);
   a.use_ring = 0;
+  a.nscenes = p.nscenes > 1 ? p.nscenes : 1;
+  a.bps = 1;
+  a.seed_stride = p.seed_stride;
+  a.out_stride = a.n_samples * 3;
+  a.adj_stride = (uint64_t)p.width * p.height * 3;
   a.rc_spp = (p.spp > 0 && p.spp <= (1 << 24) && (p.spp & (p.spp - 1)) == 0) ? 1.0f / (float)p.spp : 0.f;
   return a;
 }
@@ -1497,8 +1534,13 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
   }
   if (resident_grid<MODE, SPEC, BVH>(s, lds, &grid)) return -1;
   if (a.n_samples == 0) return 0;
+  TraceArgs b = a;
+  if (a.nscenes > 1) {  // scene batch: an equal share of the resident blocks per material set
+    b.bps = std::max(1, grid / a.nscenes);
+    grid = b.bps * a.nscenes;
+  }
   hipLaunchKernelGGL((trace_kernel<MODE, SPEC, BVH>), dim3(grid), dim3(block_threads<BVH>()), lds, st, s->isect, s->pairs, s->geom,
-                     s->mat, s->bnodes, s->bpairs, kd_dev ? kd_dev : s->kd, s->emit_tri, s->emit_cdf, s->emit_pmf, a,
+                     s->mat, s->bnodes, s->bpairs, kd_dev ? kd_dev : s->kd, s->emit_tri, s->emit_cdf, s->emit_pmf, b,
                      out, adj, grad, target, edges);
   HIP_TRY(hipGetLastError());
   return 0;
@@ -1515,16 +1557,35 @@ __global__ __launch_bounds__(kBlock) void kdpi_kernel(const float *__restrict__ 
   if (i < n) out[i] = kd[i] / kPiF;
 }
 
+// Per-launch scratch (the fused render's sample buffer, kd/pi of large
+// scenes) is allocated in stream order on the launch's own stream and freed
+// behind it: launches on different streams never share a buffer, and the
+// device's default pool (release threshold raised in gpu_upload) recycles
+// the blocks without a device-wide synchronisation.
+struct StreamScratch {
+  void *p = nullptr;
+  hipStream_t st = nullptr;
+  int alloc(size_t bytes, hipStream_t stream) {
+    st = stream;
+    HIP_TRY(hipMallocAsync(&p, std::max<size_t>(bytes, 16), st));
+    return 0;
+  }
+  ~StreamScratch() {
+    if (p) (void)hipFreeAsync(p, st);
+  }
+};
+
 template <int MODE>
 static int launch(GpuScene *s, TraceArgs a, size_t lds, const float *kd_dev, float *out, const float *adj,
                   double *grad, const uint8_t *target, double *edges, hipStream_t st) {
+  StreamScratch kdpi;
   if (MODE != MODE_GRAPH && !a.kd_tables && a.n_samples > 0) {
-    const int n = 3 * s->host.nT;
-    if (!s->kdpi) HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s->kdpi), (size_t)n * sizeof(float)));
+    const int n = 3 * s->host.nT * a.nscenes;
+    if (kdpi.alloc((size_t)n * sizeof(float), st)) return -1;
     hipLaunchKernelGGL(kdpi_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, kd_dev ? kd_dev : s->kd, n,
-                       s->kdpi);
+                       (float *)kdpi.p);
     HIP_TRY(hipGetLastError());
-    a.kdpi_g = s->kdpi;
+    a.kdpi_g = (const float *)kdpi.p;
   }
   a.use_ring = 0;
   if (!use_bvh(s) && ring_on<MODE, false>()) {  // camera-ray rings after the records, if residency allows
@@ -1561,17 +1622,6 @@ int gpu_pixel_mean(const float *samples_dev, int64_t npix, int spp, float *hdr_d
   return 0;
 }
 
-static int ensure_ws(GpuScene *s, size_t bytes) {
-  if (bytes > s->ws_bytes) {
-    if (s->ws) HIP_TRY(hipFree(s->ws));
-    s->ws = nullptr;
-    s->ws_bytes = 0;
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s->ws), bytes));
-    s->ws_bytes = bytes;
-  }
-  return 0;
-}
-
 int gpu_render_samples_sm(GpuScene *s, const RenderParams &p, const float *kd_dev, float *samples_dev,
                           void *stream) {
   if (check_params(s, p)) return -1;
@@ -1581,23 +1631,30 @@ int gpu_render_samples_sm(GpuScene *s, const RenderParams &p, const float *kd_de
                           (hipStream_t)stream);
 }
 
-int gpu_pixel_mean_sm(const float *samples_dev, int64_t npix, int spp, float *hdr_dev, uint8_t *ldr_dev,
-                      void *stream) {
-  if (npix <= 0) return 0;
+static int pixel_mean_sm_sets(const float *samples_dev, int64_t npix, int spp, int nsets, float *hdr_dev,
+                              uint8_t *ldr_dev, void *stream) {
+  if (npix <= 0 || nsets <= 0) return 0;
   const int blocks = (int)((npix + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(pixel_mean_sm_kernel, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, samples_dev, npix,
-                     spp, hdr_dev, ldr_dev);
+  hipLaunchKernelGGL(pixel_mean_sm_kernel, dim3(blocks, nsets), dim3(kBlock), 0, (hipStream_t)stream, samples_dev,
+                     npix, spp, hdr_dev, ldr_dev);
   HIP_TRY(hipGetLastError());
   return 0;
+}
+
+int gpu_pixel_mean_sm(const float *samples_dev, int64_t npix, int spp, float *hdr_dev, uint8_t *ldr_dev,
+                      void *stream) {
+  return pixel_mean_sm_sets(samples_dev, npix, spp, 1, hdr_dev, ldr_dev, stream);
 }
 
 int gpu_render(GpuScene *s, const RenderParams &p, const float *kd_dev, float *hdr_dev, uint8_t *ldr_dev,
                void *stream) {
   if (check_params(s, p)) return -1;
   const int64_t npix = (int64_t)(p.row_end - p.row_begin) * p.width;
-  if (ensure_ws(s, (size_t)npix * p.spp * 3 * sizeof(float))) return -1;
-  if (gpu_render_samples_sm(s, p, kd_dev, s->ws, stream)) return -1;
-  return gpu_pixel_mean_sm(s->ws, npix, p.spp, hdr_dev, ldr_dev, stream);
+  const int sets = p.nscenes > 1 ? p.nscenes : 1;
+  StreamScratch ws;
+  if (ws.alloc((size_t)sets * npix * p.spp * 3 * sizeof(float), (hipStream_t)stream)) return -1;
+  if (gpu_render_samples_sm(s, p, kd_dev, (float *)ws.p, stream)) return -1;
+  return pixel_mean_sm_sets((const float *)ws.p, npix, p.spp, sets, hdr_dev, ldr_dev, stream);
 }
 
 int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const float *adj_dev, double *grad_dev,

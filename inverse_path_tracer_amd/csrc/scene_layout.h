@@ -152,6 +152,11 @@ struct RenderParams {
   int max_bounces;      // < 0: unbounded (reference semantics)
   uint64_t seed;
   int row_begin, row_end;
+  // scene batch: nscenes material sets over this geometry in one launch,
+  // set b with seed + b * seed_stride (kd, outputs, adjoint image, gradient
+  // at per-set strides)
+  int nscenes = 1;
+  uint64_t seed_stride = 0;
 };
 
 }  // namespace ipt

@@ -69,7 +69,8 @@ def graph_sharded(scene, target, width: int, height: int, spp: int, max_bounces=
     compressed (nT+1)*nT*7 floats, identical on every rank and equal to the
     single-GPU result up to fp64 summation order.  `scene` is a Scene (or any
     object with .nT and .graph(target, W, H, spp, mb, seed, row_begin, row_end)
-    returning (bins, data))."""
+    returning (bins, data)).  `device` is where the all-reduce runs: default
+    CPU under gloo, the current GPU under nccl (RCCL)."""
     import numpy as np
 
     from .scene import compress
@@ -78,6 +79,8 @@ def graph_sharded(scene, target, width: int, height: int, spp: int, max_bounces=
     b, e = shard_rows(height, W, R)
     bins, _ = scene.graph(target, width, height, spp, max_bounces, seed, b, e)
     t = torch.from_numpy(np.ascontiguousarray(bins, np.float64))
+    if device is None and W > 1 and dist.get_backend() == "nccl":
+        device = torch.device("cuda", torch.cuda.current_device())  # RCCL reduces device tensors only
     if device is not None:
         t = t.to(device)
     allreduce_(t)

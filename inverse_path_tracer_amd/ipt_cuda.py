@@ -1,15 +1,23 @@
-"""Drop-in replacement for the reference's ipt_cuda.py (FFI + scene files).
+"""Module surface of the reference's ipt_cuda.py, as a thin shim.
 
-Same module-level names, argument meaning and buffer layouts as
-/root/reference/ipt_cuda.py:1-184; the two ctypes handles ``lib_ipt`` and
-``lib_pt`` point at the MI355X library (lib/libipt_amd.so, which exports all
-six reference symbols) instead of ./build/libipt.so and ./build/libpt.so.
-Like the reference, the ctypes handles carry no argtypes and scene paths are
-resolved relative to the current working directory.
+Callers of /root/reference/ipt_cuda.py (ipt.py:7,139) find the same names,
+signatures, return values and buffer layouts here:
 
-Behavioural differences: native errors raise NativeError
-instead of killing the process with exit(1); everything else -- scene text,
-ObjParams, the createGraph output split, the materials layout -- is unchanged.
+* constants: ``lib_ipt``/``lib_pt`` (ipt_cuda.py:7-8; both are the MI355X
+  library lib/libipt_amd.so, which exports all six reference symbols), the
+  shape tags ``Cube, Sphere, Cornell, Other`` and ``c_int_p``/``c_float_p``;
+* scene text: ``rand_mtl``, ``to_string``, ``from_string``, ``load_params``,
+  ``ObjParams``, ``dereference`` (ipt_cuda.py:14-107) -- the parsing and
+  formatting live in ``scene.py``; this module only packs the results into
+  the ctypes records the legacy ``loadScene`` takes;
+* the three workflow calls ``generate_files``, ``generate_data`` and
+  ``render_with_materials`` (ipt_cuda.py:115-183), which drive the legacy C
+  symbols (createImage / createGraph render the configuration set by
+  ``ipt_legacy_config``, default 500x500, 100 spp, unbounded, time seed).
+
+Differences, all deliberate: a failing native call raises
+``NativeError`` (the reference's library exit(1)s or silently writes
+nothing); ``render_with_materials`` also accepts a numpy array.
 """
 import os
 from ctypes import POINTER, Structure, c_char_p, c_float, c_int, c_void_p, cdll, pointer
@@ -17,190 +25,159 @@ from ctypes import POINTER, Structure, c_char_p, c_float, c_int, c_void_p, cdll,
 import numpy as np
 
 from . import _native
+from .scene import format_object_block, inline_kd, parse_object_block, parse_scene_text
 
-try:  # the reference shows a tqdm progress bar in generate_files
-    from tqdm import tqdm
+try:  # the reference shows a progress bar while generating scenes
+    from tqdm import tqdm as _progress
 except Exception:  # pragma: no cover
-    def tqdm(x):
-        return x
+    def _progress(it):
+        return it
 
-_native.lib()  # fails loudly when the library is missing (no fallback)
-lib_ipt = cdll.LoadLibrary(_native.LIB_PATH)  # ipt_cuda.py:7
-lib_pt = cdll.LoadLibrary(_native.LIB_PATH)   # ipt_cuda.py:8
-(Cube, Sphere, Cornell, Other) = (0, 1, 2, 3)
-
+_native.lib()  # no library -> NativeError here (there is no fallback)
+lib_ipt = cdll.LoadLibrary(_native.LIB_PATH)
+lib_pt = lib_ipt
+Cube, Sphere, Cornell, Other = range(4)
 c_int_p = POINTER(c_int)
 c_float_p = POINTER(c_float)
 
+# shape tag -> (OBJ, fixed MTL or None = a random inline diffuse material)
+_SHAPES = {
+    Cube: ("./shapes/cube.obj", None),
+    Sphere: ("./shapes/sphere.obj", None),
+    Cornell: ("./CornellBox/CornellBox-Empty-CO.obj", "./CornellBox/CornellBox-Empty-CO.mtl"),
+}
+
 
 def rand_mtl():
-    """ipt_cuda.py:14-15"""
-    return f"""*Kd {np.random.uniform()} {np.random.uniform()} {np.random.uniform()}*"""
+    """Inline material with three uniform draws from numpy's global RNG."""
+    return inline_kd([np.random.uniform() for _ in range(3)])
 
 
 def to_string(shp=None, pos=None, ori=None, scl=None, obj_file=None, mtl_file=None):
-    """ipt_cuda.py:17-37"""
-    string = ""
-    if pos is not None:
-        string += f'POS {pos[0]} {pos[1]} {pos[2]}\n'
-    if ori is not None:
-        string += f'ORI {ori[0]} {ori[1]} {ori[2]}\n'
-    if scl is not None:
-        string += f'SCL {scl[0]} {scl[1]} {scl[2]}\n'
-    if shp is Cube:
-        obj_file = "./shapes/cube.obj"
-        mtl_file = rand_mtl() if mtl_file is None else mtl_file
-    elif shp is Sphere:
-        obj_file = "./shapes/sphere.obj"
-        mtl_file = rand_mtl() if mtl_file is None else mtl_file
-    elif shp is Cornell:
-        obj_file = "./CornellBox/CornellBox-Empty-CO.obj"
-        mtl_file = "./CornellBox/CornellBox-Empty-CO.mtl"
+    """One OBJECT block's text; a shape tag fixes the OBJ (and MTL) path."""
+    if shp in _SHAPES:
+        obj_file, fixed = _SHAPES[shp]
+        if fixed is not None:
+            mtl_file = fixed
+        elif mtl_file is None:
+            mtl_file = rand_mtl()
     assert obj_file is not None and mtl_file is not None
-    string += f'OBJ {obj_file}\n'
-    string += f'MTL {mtl_file}\n'
-    return string
-
-
-def from_string(string):
-    """ipt_cuda.py:39-59"""
-    lines = string.split("\n")
-    pos, ori, scl, obj_file, mtl_file = [None] * 5
-    for line in lines:
-        items = line.strip().split(" ")
-        token, values = items[0], items[1:]
-        if token == "POS":
-            pos = [float(x) for x in values]
-        elif token == "ORI":
-            ori = [float(x) for x in values]
-        elif token == "SCL":
-            scl = [float(x) for x in values]
-        elif token == "OBJ":
-            obj_file = values[0]
-        elif token == "MTL":
-            mtl_file = " ".join(values)
-    if pos is None:
-        pos = [0] * 3
-    if ori is None:
-        ori = [0] * 3
-    if scl is None:
-        scl = [1] * 3
-    assert obj_file is not None and mtl_file is not None
-    return ObjParams(pos, ori, scl, obj_file, mtl_file)
+    return format_object_block(obj_file, mtl_file, pos, ori, scl)
 
 
 class ObjParams(Structure):
-    """ipt_cuda.py:61-78"""
+    """ctypes record of one object (field layout of the reference's ObjParams)."""
 
-    _fields_ = [
-        ('shp', c_int),
-        ('pos', (c_float * 3)),
-        ('ori', (c_float * 3)),
-        ('scl', (c_float * 3)),
-        ('obj_file', c_char_p),
-        ('mtl_file', c_char_p),
-    ]
+    _fields_ = [("shp", c_int), ("pos", c_float * 3), ("ori", c_float * 3), ("scl", c_float * 3),
+                ("obj_file", c_char_p), ("mtl_file", c_char_p)]
 
     def __init__(self, pos, ori, scl, obj_file, mtl_file):
-        self.pos = (c_float * 3)(*pos)
-        self.ori = (c_float * 3)(*ori)
-        self.scl = (c_float * 3)(*scl)
-        self.obj_file = c_char_p(obj_file.encode('utf-8'))
-        self.mtl_file = c_char_p(mtl_file.encode('utf-8'))
+        super().__init__()
+        for name, v in (("pos", pos), ("ori", ori), ("scl", scl)):
+            setattr(self, name, (c_float * 3)(*v))
+        self.obj_file = c_char_p(obj_file.encode("utf-8"))
+        self.mtl_file = c_char_p(mtl_file.encode("utf-8"))
+
+
+def _record(spec):
+    return ObjParams(spec.pos, spec.ori, spec.scl, spec.obj_file, spec.mtl_file)
+
+
+def from_string(string):
+    try:
+        spec = parse_object_block(string)
+    except ValueError as e:  # the reference asserts
+        raise AssertionError(str(e))
+    return _record(spec)
 
 
 def dereference(py_objects):
-    """ipt_cuda.py:80-89"""
-    n = len(py_objects)
-    poss = (c_float_p * n)(*[o.pos for o in py_objects])
-    oris = (c_float_p * n)(*[o.ori for o in py_objects])
-    scls = (c_float_p * n)(*[o.scl for o in py_objects])
-    objs = (c_char_p * n)(*[o.obj_file for o in py_objects])
-    mtls = (c_char_p * n)(*[o.mtl_file for o in py_objects])
-    return poss, oris, scls, objs, mtls, n
+    """Parallel pointer arrays + count: loadScene's first six arguments."""
+    objs = list(py_objects)
+    n = len(objs)
+
+    def column(ctype, field):
+        return (ctype * n)(*[getattr(o, field) for o in objs])
+
+    return (column(c_float_p, "pos"), column(c_float_p, "ori"), column(c_float_p, "scl"),
+            column(c_char_p, "obj_file"), column(c_char_p, "mtl_file"), n)
 
 
 def load_params(filename):
-    """ipt_cuda.py:91-107"""
     with open(filename, "r") as f:
-        lines = f.readlines()
-    obj_params = []
-    curr = ""
-    for line in lines:
-        line = line.strip()
-        if line == "OBJECT":
-            if len(curr) > 0:
-                obj_params.append(from_string(curr))
-            curr = ""
-        else:
-            curr += line + "\n"
-    obj_params.append(from_string(curr))
-    params = dereference(obj_params)
-    return params
+        specs = parse_scene_text(f.read())
+    return dereference([_record(s) for s in specs])
+
+
+def _checked(what, rc=None):
+    err = _native.last_error()
+    if err or (rc is not None and rc < 0):
+        raise _native.NativeError("%s failed: %s" % (what, err or "error"))
+    return rc
 
 
 def load_scene(scenefile):
-    """ipt_cuda.py:109-113"""
-    params = load_params(scenefile)
-    scene_ptr = c_void_p(0)
-    n_t = lib_pt.loadScene(*params, pointer(scene_ptr))
-    if n_t < 0:
-        raise _native.NativeError("loadScene failed: %s" % _native.last_error())
-    return n_t, scene_ptr
+    """(nT, scene handle) of a scene file; paths resolve against the CWD."""
+    handle = c_void_p(0)
+    _native.lib().ipt_clear_error()
+    n_t = _checked("loadScene", lib_pt.loadScene(*load_params(scenefile), pointer(handle)))
+    return n_t, handle
+
+
+def _create_image(handle, png_path):
+    """createImage + freeScene, raising if the render or the PNG write failed."""
+    _native.lib().ipt_clear_error()
+    lib_pt.createImage(handle, c_char_p(png_path.encode("utf-8")))
+    err = _native.last_error()
+    lib_ipt.freeScene(handle)
+    if err:
+        raise _native.NativeError("createImage(%s) failed: %s" % (png_path, err))
 
 
 def generate_files(n):
-    """ipt_cuda.py:115-134: write scenes/{i}.txt (Cornell + random cube) and
-    render imgs/{i}.png."""
+    """scenes/{i}.txt (Cornell box + a cube with a random diffuse colour) and
+    imgs/{i}.png, its legacy-configuration render, for i < n."""
     os.makedirs("scenes", exist_ok=True)
     os.makedirs("imgs", exist_ok=True)
-    for i in tqdm(range(n)):
-        with open(f"scenes/{i}.txt", "w") as f:
-            f.write("OBJECT\n")
-            f.write(to_string(shp=Cornell, pos=np.array([0, 0, 4]), scl=np.ones(3) * 2))
-            f.write("OBJECT\n")
-            f.write(to_string(shp=Cube, pos=np.array([0, -1.5, 4])))
-        n_t, scene_ptr = load_scene(f'scenes/{i}.txt')
-        filename_ptr = c_char_p(f'imgs/{i}.png'.encode('utf-8'))
-        lib_pt.createImage(scene_ptr, filename_ptr)
-        lib_ipt.freeScene(scene_ptr)
+    for i in _progress(range(n)):
+        text = ("OBJECT\n" + to_string(shp=Cornell, pos=np.array([0, 0, 4]), scl=np.ones(3) * 2) +
+                "OBJECT\n" + to_string(shp=Cube, pos=np.array([0, -1.5, 4])))
+        path = "scenes/%d.txt" % i
+        with open(path, "w") as f:
+            f.write(text)
+        _, handle = load_scene(path)
+        _create_image(handle, "imgs/%d.png" % i)
 
 
 def generate_data(scenefile, imgfile):
-    """ipt_cuda.py:136-165: transport graph + labels of one scene."""
-    len_data = 7
-    n_t, scene_ptr = load_scene(scenefile)
-    filename_ptr = c_char_p(imgfile.encode('utf-8'))
-    size = (n_t + 1) * n_t
-    data_sz = size * len_data
-    data = (c_float * data_sz)(0)
+    """createGraph against imgfile + getMaterials: (w (nT+1, nT),
+    pixel (nT+1, nT, 3), light (nT+1, nT, 3), labels (nT, 3)), float64."""
+    n_t, handle = load_scene(scenefile)
+    rows = (n_t + 1) * n_t
+    flat = np.zeros(rows * 7, np.float32)
+    labels = np.zeros(n_t * 3, np.float32)
     _native.lib().ipt_clear_error()
-    lib_ipt.createGraph(scene_ptr, filename_ptr, data)
+    lib_ipt.createGraph(handle, c_char_p(imgfile.encode("utf-8")), flat.ctypes.data_as(c_float_p))
     err = _native.last_error()
-    labels = (c_float * (n_t * 3))(0)
-    lib_ipt.getMaterials(scene_ptr, labels)
-    labels = np.ctypeslib.as_array(labels).astype(np.float64).reshape(n_t, 3)
-    lib_ipt.freeScene(scene_ptr)
+    lib_ipt.getMaterials(handle, labels.ctypes.data_as(c_float_p))
+    lib_ipt.freeScene(handle)
     if err:
         raise _native.NativeError("createGraph failed: %s" % err)
-    data = np.ctypeslib.as_array(data).astype(np.float64)
-    w = data[:size].reshape(n_t + 1, n_t)
-    pixel = data[size:size * 4].reshape(n_t + 1, n_t, 3)
+    w, pixel, light = np.split(flat.astype(np.float64), [rows, 4 * rows])
+    pixel = pixel.reshape(n_t + 1, n_t, 3)
     assert not np.isnan(pixel).any()
-    light = data[size * 4:].reshape(n_t + 1, n_t, 3)
-    return w, pixel, light, labels
+    return w.reshape(n_t + 1, n_t), pixel, light.reshape(n_t + 1, n_t, 3), labels.astype(np.float64).reshape(n_t, 3)
 
 
 def render_with_materials(scenefile, imgfile, materials):
-    """ipt_cuda.py:167-183 (materials: a torch tensor or array, (nT, 3))."""
-    params = load_params(scenefile)
-    scene_ptr = c_void_p(0)
-    filename_ptr = c_char_p(imgfile.encode('utf-8'))
-    n_t = lib_pt.loadScene(*params, pointer(scene_ptr))
-    if n_t < 0:
-        raise _native.NativeError("loadScene failed: %s" % _native.last_error())
-    arr = materials.numpy() if hasattr(materials, "numpy") else np.asarray(materials)
-    arr = np.ascontiguousarray(arr.astype(np.float32))
-    lib_ipt.setMaterials(scene_ptr, arr.ctypes.data_as(c_float_p))
-    lib_pt.createImage(scene_ptr, filename_ptr)
-    lib_ipt.freeScene(scene_ptr)
+    """Legacy-configuration render of scenefile with per-triangle diffuse
+    albedo `materials` (nT, 3) (torch tensor or array) written to imgfile."""
+    _, handle = load_scene(scenefile)
+    kd = materials.detach().cpu().numpy() if hasattr(materials, "detach") else np.asarray(materials)
+    kd = np.ascontiguousarray(kd, np.float32)
+    lib_ipt.setMaterials(handle, kd.ctypes.data_as(c_float_p))
+    err = _native.last_error()
+    if err:
+        lib_ipt.freeScene(handle)
+        raise _native.NativeError("setMaterials failed: %s" % err)
+    _create_image(handle, imgfile)

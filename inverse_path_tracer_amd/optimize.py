@@ -7,13 +7,23 @@ minimises the L2 distance between the rendered HDR image and a target render
 (the reference's imgs/*.png are not shipped; targets are forward renders at
 the ground-truth Kd with many more samples).
 
-Scene-parallel: scene i belongs to rank i % world; per-scene parameters need
-no collective.  ``tie_shared=True`` additionally treats the Cornell-box
-triangles (identical in every scenes/*.txt) as ONE parameter set shared by all
-scenes -- their gradient is then summed across scenes and ranks with a single
-RCCL all-reduce per step.
+* Scene batches: scenes/0..99.txt share their geometry and differ only in the
+  cube's Kd (ipt_cuda.py:115-134 writes them that way), so the scenes of a rank
+  form ONE batch over one loaded geometry: each step is one batched forward
+  launch and one batched adjoint launch (torch_ops.render_batch) for all of
+  them, instead of two launches and an autograd graph per scene.  Scenes whose
+  geometry differs fall back to per-scene renders.
+* Unbiased gradients: the adjoint of step t traces an independent sample
+  stream (``adjoint_seed``), so the residual I - T of the forward is not
+  correlated with the derivative (same-stream replay biases Adam towards
+  darker albedo by O(1/spp)).
+* Scene-parallel: scene i belongs to rank i % world; per-scene parameters need
+  no collective.  ``tie_shared=k`` additionally treats the first k triangles
+  (18 = the Cornell box, identical in every scene) as ONE parameter set shared
+  by all scenes -- their gradient is summed across scenes and ranks with a
+  single RCCL all-reduce per step.
 
-    python -m inverse_path_tracer_amd.optimize --scenes assets/scenes --n 4 --steps 50
+    python -m inverse_path_tracer_amd.optimize --scenes assets/scenes --n 13 --steps 200
 """
 from __future__ import annotations
 
@@ -23,20 +33,25 @@ import time
 from dataclasses import dataclass, field
 from typing import List, Optional
 
+import numpy as np
 import torch
 
 from . import torch_ops
 from .distributed import allreduce_, world
 from .scene import Scene
 
+# ipt_scene_export_triangles columns holding the diffuse Kd (everything else
+# is geometry / other material fields that must agree for a batch)
+_KD_COLS = slice(25, 28)
+
 
 @dataclass
 class SceneTask:
     path: str
-    scene: Scene
+    scene: Scene                  # geometry handle (shared by the tasks of one batch)
     truth: torch.Tensor           # ground-truth Kd (nT, 3)
     target: torch.Tensor          # target HDR image (H, W, 3)
-    kd: torch.Tensor              # parameters (nT, 3), requires_grad
+    kd: torch.Tensor              # parameters (nT, 3)
     history: List[float] = field(default_factory=list)
 
 
@@ -44,65 +59,154 @@ def _scene_files(root: str, n: int) -> List[str]:
     return [os.path.join(root, "%d.txt" % i) for i in range(n)]
 
 
+def _geometry_key(sc: Scene) -> bytes:
+    t = sc.triangles()
+    return np.concatenate([t[:, :_KD_COLS.start], t[:, _KD_COLS.stop:]], axis=1).tobytes()
+
+
 def build_tasks(files: List[str], width: int, height: int, target_spp: int, max_bounces: int, init: float,
-                device: torch.device, seed: int = 7) -> List[SceneTask]:
+                device: torch.device, seed: int = 7, target_chunk: int = 16) -> List[SceneTask]:
+    """Load the scenes (one device geometry per distinct geometry), render the
+    targets in batches of `target_chunk`, and create the parameters."""
+    groups = {}  # geometry key -> device Scene
     tasks = []
     for f in files:
-        sc = Scene.from_file(f)
-        truth = torch.tensor(sc.materials, device=device)
-        with torch.no_grad():
-            target = torch_ops.render(sc, truth, width, height, target_spp, max_bounces, seed=seed + 10**9)
-        kd = torch.full_like(truth, init).requires_grad_(True)
-        tasks.append(SceneTask(f, sc, truth, target, kd))
+        host = Scene.from_file(f, device=False)
+        key = _geometry_key(host)
+        if key not in groups:
+            groups[key] = Scene.from_file(f)
+        truth = torch.tensor(host.materials, device=device)
+        host.close()
+        tasks.append(SceneTask(f, groups[key], truth, None, torch.full_like(truth, init).requires_grad_(True)))
+    stride = width * height * target_spp
+    with torch.no_grad():
+        for sc in groups.values():
+            mine = [i for i, t in enumerate(tasks) if t.scene is sc]
+            for c in range(0, len(mine), target_chunk):
+                idx = mine[c:c + target_chunk]
+                kd = torch.stack([tasks[i].truth for i in idx])
+                img = torch_ops.render_batch(sc, kd, width, height, target_spp, max_bounces,
+                                             seed=seed + 10**9 + idx[0] * stride, seed_stride=stride)
+                for j, i in enumerate(idx):
+                    tasks[i].target = img[j].clone()
     return tasks
 
 
-def optimize(tasks: List[SceneTask], width: int, height: int, spp: int, max_bounces: int, steps: int,
-             lr: float = 1e-2, tie_shared: Optional[int] = None, seed: int = 0, log_every: int = 0):
-    """Adam on every task's kd.  tie_shared = number of leading triangles whose
-    Kd is shared by all scenes (18 = the Cornell box), or None."""
-    W, R = world()
-    shared = None
-    if tie_shared:
-        shared = tasks[0].kd.detach()[:tie_shared].clone().requires_grad_(True) if tasks else None
-        if shared is None:
-            shared = torch.full((tie_shared, 3), 0.5, device="cuda", requires_grad=True)
-    params = [t.kd for t in tasks] + ([shared] if shared is not None else [])
-    opt = torch.optim.Adam(params, lr=lr)
-    pending = []  # (task, loss tensor) in step order
-    for step in range(steps):
-        opt.zero_grad(set_to_none=False)
-        for i, t in enumerate(tasks):
-            kd = t.kd
-            if shared is not None:
-                kd = torch.cat([shared, t.kd[tie_shared:]], dim=0)
-            img = torch_ops.render(t.scene, kd, width, height, spp, max_bounces,
-                                   seed=seed + (step * 1009 + i) * width * height * spp)
-            loss = ((img - t.target) ** 2).mean()
-            loss.backward()
-            pending.append((t, loss.detach()))  # no host sync per scene: read back once per step
-        if shared is not None:
-            if shared.grad is None:
-                shared.grad = torch.zeros_like(shared)
-            allreduce_(shared.grad)  # the only exchange: one nT_shared*3 all-reduce
-        opt.step()
+class MaterialOptimizer:
+    """Persistent Adam state over every task's kd (nT, 3).  Each group of
+    tasks sharing a geometry is one batch: a (S, nT, 3) parameter whose rows
+    the tasks' kd become views of, rendered by one batched forward and one
+    batched adjoint launch per step.  tie_shared = number of leading
+    triangles whose Kd is shared by all scenes (18 = the Cornell box), or
+    None.  Losses reach the tasks' histories with one device->host copy every
+    `flush_every` steps (on every rank) and at the end of each run()."""
+
+    def __init__(self, tasks: List[SceneTask], width: int, height: int, spp: int, max_bounces: int,
+                 lr: float = 1e-2, tie_shared: Optional[int] = None, seed: int = 0, flush_every: int = 16,
+                 decorrelate: bool = True):
+        self.tasks, self.W, self.H, self.spp, self.mb = tasks, width, height, spp, max_bounces
+        self.tie, self.seed, self.flush_every, self.decorrelate = tie_shared, seed, flush_every, decorrelate
+        self.frame = width * height * spp
+        self.batches = []  # (scene, tasks)
+        for t in tasks:
+            for b in self.batches:
+                if b[0] is t.scene:
+                    b[1].append(t)
+                    break
+            else:
+                self.batches.append((t.scene, [t]))
+        self.leaves, self.targets, self.offsets = [], [], []
+        for sc, ts in self.batches:
+            leaf = torch.stack([t.kd.detach() for t in ts]).clone().requires_grad_(True)
+            tgt = torch.stack([t.target for t in ts])
+            for j, t in enumerate(ts):
+                t.kd, t.target = leaf[j], tgt[j]
+            self.offsets.append(sum(len(b[1]) for b in self.batches[:len(self.leaves)]))
+            self.leaves.append(leaf)
+            self.targets.append(tgt)
+        self.shared = None
+        if tie_shared:
+            self.shared = tasks[0].kd.detach()[:tie_shared].clone().requires_grad_(True) if tasks else \
+                torch.full((tie_shared, 3), 0.5, device="cuda", requires_grad=True)
+        self.params = self.leaves + ([self.shared] if self.shared is not None else [])
+        self.opt = torch.optim.Adam(self.params, lr=lr)
+        self.step_count = 0
+        self.pending = []  # (tasks, per-scene loss tensor) in step order
+
+    def step(self):
+        """One Adam step over every scene (no host synchronisation)."""
+        self.opt.zero_grad(set_to_none=False)
+        step = self.step_count
+        for (sc, ts), leaf, target, n_before in zip(self.batches, self.leaves, self.targets, self.offsets):
+            kd = leaf
+            if self.shared is not None:
+                kd = torch.cat([self.shared.unsqueeze(0).expand(len(ts), -1, -1), leaf[:, self.tie:]], dim=1)
+            base = self.seed + (step * len(self.tasks) + n_before) * self.frame
+            img = torch_ops.render_batch(sc, kd, self.W, self.H, self.spp, self.mb, seed=base, seed_stride=self.frame,
+                                         adjoint_seed=(base + (1 << 62)) if self.decorrelate else None)
+            per_scene = ((img - target) ** 2).mean(dim=(1, 2, 3))
+            per_scene.sum().backward()  # each scene's loss only reaches its own parameters
+            self.pending.append((ts, per_scene.detach()))
+        if self.shared is not None:
+            if self.shared.grad is None:
+                self.shared.grad = torch.zeros_like(self.shared)
+            allreduce_(self.shared.grad)  # the only exchange: one nT_shared*3 all-reduce
+        self.opt.step()
         with torch.no_grad():
-            for p in params:
+            for p in self.params:
                 p.clamp_(0.0, 1.0)
-        if log_every and step % log_every == 0 and R == 0:
-            _flush_losses(pending)
-            print("step %d loss %.6g" % (step, sum(t.history[-1] for t in tasks) / max(1, len(tasks))), flush=True)
-    _flush_losses(pending)
-    return shared
+        self.step_count += 1
+        if self.flush_every and self.step_count % self.flush_every == 0:
+            _flush_losses(self.pending)
+
+    def run(self, steps: int, log_every: int = 0):
+        _, R = world()
+        for i in range(steps):
+            self.step()
+            if log_every and i % log_every == 0:
+                _flush_losses(self.pending)
+                if R == 0:
+                    print("step %d loss %.6g" % (self.step_count - 1, sum(t.history[-1] for t in self.tasks) /
+                                                 max(1, len(self.tasks))), flush=True)
+        _flush_losses(self.pending)
+        return self
+
+
+def optimize(tasks: List[SceneTask], width: int, height: int, spp: int, max_bounces: int, steps: int,
+             lr: float = 1e-2, tie_shared: Optional[int] = None, seed: int = 0, log_every: int = 0,
+             flush_every: int = 16, decorrelate: bool = True):
+    """`steps` Adam steps of a fresh MaterialOptimizer; returns the shared
+    (tied) parameter or None."""
+    m = MaterialOptimizer(tasks, width, height, spp, max_bounces, lr, tie_shared, seed, flush_every, decorrelate)
+    m.run(steps, log_every)
+    return m.shared
 
 
 def _flush_losses(pending):
-    """Move the step losses to the tasks' histories with one device->host copy."""
+    """Move the pending per-scene losses to the tasks' histories (one copy)."""
     if pending:
-        vals = torch.stack([l for _, l in pending]).float().cpu().tolist()
-        for (t, _), v in zip(pending, vals):
-            t.history.append(v)
+        vals = torch.cat([l for _, l in pending]).float().cpu().tolist()
+        k = 0
+        for ts, _ in pending:
+            for t in ts:
+                t.history.append(vals[k])
+                k += 1
         pending.clear()
+
+
+def observable_mask(tasks: List[SceneTask], width: int, height: int, spp: int, max_bounces: int, seed: int = 5,
+                    frac: float = 0.25, first: int = 18):
+    """Per task, the triangles >= `first` whose Kd the image constrains: |dL/dKd|
+    at the start above `frac` of the largest (the cube's back and bottom faces
+    never reach the camera and cannot be recovered)."""
+    masks = []
+    for t in tasks:
+        kd = t.kd.detach().clone().requires_grad_(True)
+        img = torch_ops.render(t.scene, kd, width, height, spp, max_bounces, seed=seed)
+        ((img - t.target) ** 2).mean().backward()
+        g = kd.grad.abs().sum(1)[first:]
+        masks.append(g > frac * float(g.max()))
+    return masks
 
 
 def main():
@@ -114,7 +218,7 @@ def main():
     ap.add_argument("--spp", type=int, default=32)
     ap.add_argument("--target-spp", type=int, default=1024)
     ap.add_argument("--bounces", type=int, default=4)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--lr", type=float, default=1e-2)
     ap.add_argument("--tie", action="store_true")
     args = ap.parse_args()

@@ -51,6 +51,20 @@ def parse_object_block(text: str) -> ObjectSpec:
                       scl if scl is not None else [1.0] * 3)
 
 
+def format_object_block(obj_file: str, mtl_file: str, pos=None, ori=None, scl=None) -> str:
+    """Inverse of parse_object_block in the reference's spelling (ipt_cuda.py:17-37
+    to_string): optional POS/ORI/SCL lines with each value printed by str(),
+    then OBJ and MTL."""
+    keys = (("POS", pos), ("ORI", ori), ("SCL", scl))
+    head = "".join("%s %s\n" % (k, " ".join(str(x) for x in v[:3])) for k, v in keys if v is not None)
+    return head + "OBJ %s\nMTL %s\n" % (obj_file, mtl_file)
+
+
+def inline_kd(kd: Sequence[float]) -> str:
+    """The inline material string ``*Kd r g b*`` (ipt_cuda.py:14-15)."""
+    return "*Kd %s*" % " ".join(str(x) for x in kd)
+
+
 def parse_scene_text(text: str) -> List[ObjectSpec]:
     """load_params (ipt_cuda.py:91-107)."""
     objects, cur = [], ""

@@ -45,12 +45,12 @@ def adjoint_band(scene: Scene, params: N.Params, kd, adj_band: torch.Tensor, gra
 
 class _RenderFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, kd, scene, params):
+    def forward(ctx, kd, scene, params, adjoint_seed):
         kd_c = kd.detach().contiguous().float()
         rows = params.row_end - params.row_begin
         hdr = torch.empty((rows, params.width, 3), device=kd.device, dtype=torch.float32)
         render_into(scene, params, kd_c, hdr)
-        ctx.scene, ctx.params = scene, params
+        ctx.scene, ctx.params, ctx.adjoint_seed = scene, params, adjoint_seed
         ctx.save_for_backward(kd_c)
         return hdr
 
@@ -58,14 +58,71 @@ class _RenderFn(torch.autograd.Function):
     def backward(ctx, grad_hdr):
         (kd_c,) = ctx.saved_tensors
         g = torch.zeros(kd_c.shape, device=kd_c.device, dtype=torch.float64)
-        adjoint_band(ctx.scene, ctx.params, kd_c, grad_hdr.float(), g)
-        return g.to(kd_c.dtype), None, None
+        adjoint_band(ctx.scene, _replay_params(ctx.params, ctx.adjoint_seed), kd_c, grad_hdr.float(), g)
+        return g.to(kd_c.dtype), None, None, None
+
+
+def _replay_params(p: N.Params, adjoint_seed):
+    """The adjoint's parameters: the forward's (common random numbers: the
+    exact derivative of the returned image), or the same configuration on an
+    independent sample stream (adjoint_seed: an unbiased estimate of the
+    derivative of the expected image, uncorrelated with the forward's noise)."""
+    if adjoint_seed is None:
+        return p
+    return N.Params(p.width, p.height, p.spp, p.max_bounces, int(adjoint_seed) & 0xFFFFFFFFFFFFFFFF, p.row_begin,
+                    p.row_end)
 
 
 def render(scene: Scene, kd: torch.Tensor, width: int, height: int, spp: int, max_bounces=4, seed: int = 0,
-           row_begin: int = 0, row_end=None) -> torch.Tensor:
-    """Differentiable render: HDR image of rows [row_begin, row_end) w.r.t. kd."""
+           row_begin: int = 0, row_end=None, adjoint_seed=None) -> torch.Tensor:
+    """Differentiable render: HDR image of rows [row_begin, row_end) w.r.t. kd.
+
+    The backward pass replays the forward's paths (adjoint_seed None) or
+    traces the same configuration with seed `adjoint_seed`.  The second form
+    is what an optimiser of E[loss] wants: with the forward's own samples the
+    gradient of (I - T)^2 correlates the residual with the derivative, a bias
+    of order 1/spp towards darker albedo."""
     if max_bounces is None and kd.requires_grad:
         raise ValueError("the adjoint needs a finite max_bounces (vertex records live in LDS)")
     p = N.make_params(width, height, spp, max_bounces, seed, row_begin, row_end)
-    return _RenderFn.apply(kd, scene, p)
+    return _RenderFn.apply(kd, scene, p, adjoint_seed)
+
+
+class _BatchRenderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, kd, scene, params, stride, adjoint_seed):
+        kd_c = kd.detach().contiguous().float()
+        S = kd_c.shape[0]
+        hdr = torch.empty((S, params.height, params.width, 3), device=kd.device, dtype=torch.float32)
+        N.check(N.lib().ipt_render_batch_dev(scene.handle, C.byref(params), S, stride, kd_c.data_ptr(),
+                                             hdr.data_ptr(), _stream(hdr.device)), "ipt_render_batch_dev")
+        ctx.scene, ctx.params, ctx.stride, ctx.adjoint_seed = scene, params, stride, adjoint_seed
+        ctx.save_for_backward(kd_c)
+        return hdr
+
+    @staticmethod
+    def backward(ctx, grad_hdr):
+        (kd_c,) = ctx.saved_tensors
+        g = torch.zeros(kd_c.shape, device=kd_c.device, dtype=torch.float64)
+        adj = grad_hdr.float().contiguous()
+        p = _replay_params(ctx.params, ctx.adjoint_seed)
+        N.check(N.lib().ipt_adjoint_batch_dev(ctx.scene.handle, C.byref(p), kd_c.shape[0], ctx.stride,
+                                              kd_c.data_ptr(), adj.data_ptr(), g.data_ptr(), _stream(g.device)),
+                "ipt_adjoint_batch_dev")
+        return g.to(kd_c.dtype), None, None, None, None
+
+
+def render_batch(scene: Scene, kd: torch.Tensor, width: int, height: int, spp: int, max_bounces=4, seed: int = 0,
+                 seed_stride=None, adjoint_seed=None) -> torch.Tensor:
+    """Differentiable render of S material sets over one geometry in one
+    launch (ipt_render_batch_dev): kd (S, nT, 3) -> HDR images (S, H, W, 3).
+    Set b is ``render(scene, kd[b], ..., seed + b * seed_stride)`` bit for bit
+    (default stride: one frame of samples, so the sets' sample streams are
+    disjoint); the backward runs ONE batched adjoint launch."""
+    if max_bounces is None and kd.requires_grad:
+        raise ValueError("the adjoint needs a finite max_bounces (vertex records live in LDS)")
+    if kd.dim() != 3 or kd.shape[1] != scene.nT or kd.shape[2] != 3:
+        raise ValueError("kd must be (S, nT=%d, 3), got %s" % (scene.nT, tuple(kd.shape)))
+    stride = width * height * spp if seed_stride is None else int(seed_stride)
+    p = N.make_params(width, height, spp, max_bounces, seed)
+    return _BatchRenderFn.apply(kd, scene, p, stride, adjoint_seed)
