@@ -141,9 +141,11 @@ class MaterialOptimizer:
             kd = leaf
             if self.shared is not None:
                 kd = torch.cat([self.shared.unsqueeze(0).expand(len(ts), -1, -1), leaf[:, self.tie:]], dim=1)
-            base = self.seed + (step * len(self.tasks) + n_before) * self.frame
+            # step t uses 2T frames of the sample-index space: the T forward frames, then the T adjoint frames
+            T = len(self.tasks)
+            base = self.seed + (2 * step * T + n_before) * self.frame
             img = torch_ops.render_batch(sc, kd, self.W, self.H, self.spp, self.mb, seed=base, seed_stride=self.frame,
-                                         adjoint_seed=(base + (1 << 62)) if self.decorrelate else None)
+                                         adjoint_seed=(base + T * self.frame) if self.decorrelate else None)
             per_scene = ((img - target) ** 2).mean(dim=(1, 2, 3))
             per_scene.sum().backward()  # each scene's loss only reaches its own parameters
             self.pending.append((ts, per_scene.detach()))

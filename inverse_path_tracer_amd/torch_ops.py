@@ -81,7 +81,15 @@ def render(scene: Scene, kd: torch.Tensor, width: int, height: int, spp: int, ma
     traces the same configuration with seed `adjoint_seed`.  The second form
     is what an optimiser of E[loss] wants: with the forward's own samples the
     gradient of (I - T)^2 correlates the residual with the derivative, a bias
-    of order 1/spp towards darker albedo."""
+    of order 1/spp towards darker albedo.
+
+    Choose `adjoint_seed` so that its samples' seeds (adjoint_seed + global
+    sample index) differ from the forward's in the LOW 32 bits, e.g. the
+    next frame: seed + W*H*spp.  curand_init's XORWOW set-up hashes the two
+    32-bit halves of a seed separately, so seeds equal mod 2^32 share three
+    of the five state words and their first draws differ only by a constant
+    -- correlated streams (measured: a residual bias of ~14% of the
+    same-stream one, tests/test_gpu_full.py)."""
     if max_bounces is None and kd.requires_grad:
         raise ValueError("the adjoint needs a finite max_bounces (vertex records live in LDS)")
     p = N.make_params(width, height, spp, max_bounces, seed, row_begin, row_end)
