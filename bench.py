@@ -6,8 +6,10 @@ box, 64 spp, 4 bounces (BASELINE.json configs[1]) on N MI355X.
 
 A step is one C2 frame, tiled across the ranks exactly as the north_star asks
 ("image tiles shard across the GPUs, RCCL reduce on the per-material gradient
-vector only"): rank r traces row band r of the SAME frame (shard_rows; sample
-seeds are global indices, so the bands are the single-GPU frame's samples);
+vector only"): rank r traces rows r, r + N, ... of the SAME frame
+(shard_rows_interleaved -- contiguous bands differ in cost by up to 7.6%,
+see `bands_*`; sample seeds are global indices, so the shares are the
+single-GPU frame's samples);
 the forward needs no collective, the adjoint step ends with ONE all-reduce of
 the nT*3 fp64 gradient.  Strong scaling: value = frame samples * K / (max
 over ranks of the time of K steps).  Inputs are resident in HBM before the
@@ -34,7 +36,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from inverse_path_tracer_amd import _native as N  # noqa: E402
-from inverse_path_tracer_amd.distributed import frame_seed, shard_rows  # noqa: E402
+from inverse_path_tracer_amd.distributed import frame_seed, shard_rows, shard_rows_interleaved  # noqa: E402
 from inverse_path_tracer_amd.scene import ObjectSpec, Scene  # noqa: E402
 
 W = H = 512
@@ -171,12 +173,13 @@ class Leg:
     """One workload on one scene: forward (sample-major buffer + pixel mean)
     and adjoint (+ gradient all-reduce) over rows [b, e)."""
 
-    def __init__(self, cx, objs, w, h, spp, mb, b=0, e=None, seed=0):
+    def __init__(self, cx, objs, w, h, spp, mb, b=0, e=None, seed=0, step=1):
         self.cx, self.w, self.h, self.spp, self.mb, self.seed = cx, w, h, spp, mb, seed
-        self.b, self.e = b, (h if e is None else e)
+        self.b, self.e, self.step = b, (h if e is None else e), step
+        self.rows = len(range(self.b, self.e, self.step))
         self.sc = Scene(objs)
         dev = cx.dev
-        npix = (self.e - self.b) * w
+        npix = self.rows * w
         self.npix = npix
         self.samples = torch.empty((npix * spp, 3), device=dev, dtype=torch.float32)
         self.hdr = torch.empty((npix, 3), device=dev, dtype=torch.float32)
@@ -186,7 +189,7 @@ class Leg:
 
     def params(self, step):
         return N.make_params(self.w, self.h, self.spp, self.mb, frame_seed(self.seed, step, self.w, self.h, self.spp),
-                             self.b, self.e)
+                             self.b, self.e, self.step)
 
     def fwd(self, step, ev=None):
         cx, p = self.cx, self.params(step)
@@ -207,24 +210,24 @@ class Leg:
             dist.all_reduce(self.grad)  # the per-material gradient vector, nT*3 fp64 (720 B for 30 triangles)
 
     def samples_per_call(self):
-        return (self.e - self.b) * self.w * self.spp
+        return self.rows * self.w * self.spp
 
     def close(self):
         self.sc.close()
 
 
-def band_table(cx, objs, w, h, spp, mb, n=8, reps=2):
-    """Each of the n row bands of one frame timed alone (forward, adjoint): the
-    critical path of an n-GPU tile split is the slowest band."""
+def band_table(cx, objs, w, h, spp, mb, n=8, reps=2, interleaved=False):
+    """Each of the n row shares of one frame timed alone (forward, adjoint):
+    the critical path of an n-GPU tile split is the slowest share."""
     rows = []
     for r in range(n):
-        b, e = shard_rows(h, n, r)
-        leg = Leg(cx, objs, w, h, spp, mb, b, e)
+        b, e, st = shard_rows_interleaved(h, n, r) if interleaved else shard_rows(h, n, r) + (1,)
+        leg = Leg(cx, objs, w, h, spp, mb, b, e, step=st)
         leg.fwd(10**6)
         leg.adjoint(10**6, reduce=False)
         f = cx.timed(lambda i: leg.fwd(i), reps) / reps
         a = cx.timed(lambda i: leg.adjoint(i, reduce=False), reps) / reps
-        rows.append({"rows": [b, e], "fwd_ms": round(f, 4), "adj_ms": round(a, 4)})
+        rows.append({"rows": [b, e, st], "fwd_ms": round(f, 4), "adj_ms": round(a, 4)})
         leg.close()
     fw = [x["fwd_ms"] for x in rows]
     ad = [x["adj_ms"] for x in rows]
@@ -242,8 +245,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
     cx = Ctx(dev, world, rank)
-    b, e = shard_rows(H, world, rank)
-    head = Leg(cx, CORNELL, W, H, SPP, BOUNCES, b, e, seed=args.seed)
+    b, e, rs = shard_rows_interleaved(H, world, rank)
+    head = Leg(cx, CORNELL, W, H, SPP, BOUNCES, b, e, seed=args.seed, step=rs)
     for i in range(args.warmup):
         head.fwd(10**6 + i)
         head.adjoint(10**6 + i)
@@ -279,8 +282,9 @@ def main():
                 ("c3", SCENE0, W, H, SPP, BOUNCES, "C3: scenes/0.txt (Cornell + cube, 30 triangles), 512x512, 64 spp, 4 bounces"),
                 ("bvh_sphere", SPHERE, W, H, SPP, BOUNCES, "Cornell + sphere.obj (1298 triangles, BVH), 512x512, 64 spp, 4 bounces"),
                 ("c4", SCENE0, 1024, 1024, 256, 8, "C4: scenes/0.txt, 1024x1024, 256 spp, 8 bounces")):
-            bb, ee = shard_rows(h, world, rank) if key != "c4" else shard_rows(h, 8, rank) if world <= 8 else (0, 0)
-            leg = Leg(cx, objs, w, h, spp, mb, bb, ee)
+            bb, ee, ss = shard_rows_interleaved(h, world if key != "c4" else 8, rank) if (key != "c4" or world <= 8) \
+                else (0, 0, 1)
+            leg = Leg(cx, objs, w, h, spp, mb, bb, ee, step=ss)
             leg.fwd(10**6)
             leg.adjoint(10**6)
             reps = 2 if key == "c4" else 5
@@ -290,12 +294,15 @@ def main():
             extra[key] = {"value": round(n / f / 1e3, 2), "unit": "Msamples/s", "grad_value": round(n / a / 1e3, 2),
                           "grad_unit": "grad-Msamples/s", "fwd_ms": round(f, 4), "adj_ms": round(a, 4),
                           "triangles": leg.sc.nT, "accel": leg.sc.bvh_info()["accel"],
-                          "workload": desc + ("; rank k = row band k of 8 (%d of 8 bands run)" % min(world, 8)
-                                              if key == "c4" else "; tile split over %d rank(s)" % world)}
+                          "workload": desc + ("; rank k = interleaved share k of 8 (rows k, k+8, ...; %d of 8 "
+                                              "shares run)" % min(world, 8) if key == "c4" else
+                                              "; interleaved rows over %d rank(s)" % world)}
             leg.close()
         if world == 1:
             extra["bands_c2"] = band_table(cx, CORNELL, W, H, SPP, BOUNCES, reps=4)
+            extra["bands_c2_interleaved"] = band_table(cx, CORNELL, W, H, SPP, BOUNCES, reps=4, interleaved=True)
             extra["bands_c4"] = band_table(cx, SCENE0, 1024, 1024, 256, 8, reps=1)
+            extra["bands_c4_interleaved"] = band_table(cx, SCENE0, 1024, 1024, 256, 8, reps=1, interleaved=True)
             sys.path.insert(0, os.path.join(ROOT, "tools"))
             import bench_c5
             extra["c5"] = bench_c5.run(scenes=13, steps=20, warmup=3, total=23)
@@ -331,10 +338,10 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(fwd_ms / args.steps, 4), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": "C2: CornellBox-Empty-CO.obj, 512x512, 64 spp, max_bounces=4; one frame per step "
-                                   "tiled over the ranks as row bands (fwd); adjoint dL/dKd of the band + RCCL "
-                                   "all-reduce of the gradient (grad)",
+                                   "tiled over the ranks as interleaved rows (fwd); adjoint dL/dKd of the rank's rows "
+                                   "+ RCCL all-reduce of the gradient (grad)",
                        "width": W, "height": H, "spp": SPP, "max_bounces": BOUNCES, "triangles": head.sc.nT,
-                       "parallelism": "row-band tiles x%d" % world, "rank0_rows": [b, e]},
+                       "parallelism": "interleaved row tiles x%d" % world, "rank0_rows": [b, e, rs]},
             "grad_value": round(grad_value, 2), "grad_unit": "grad-Msamples/s",
             "grad_ms_per_step": round(bwd_ms / args.steps, 4),
             "wall_s_fwd_region": round(wall_fwd, 4),

@@ -62,16 +62,20 @@ void setMaterials(void *scenePtr, float *materials);
  * continuation rays and does next-event estimation at the (B+1)-th vertex.
  * Sample s of pixel (r,c) has global index (r*width + c)*spp + s and RNG
  * seed `seed + index` (curand_init(seed+index, 0, 0)).  Only rows
- * [row_begin, row_end) are traced (sharding); images cover those rows. */
+ * row_begin, row_begin + row_step, ... < row_end are traced (sharding:
+ * row_step 1 = a contiguous band, row_step = world = a rank's interleaved
+ * share); images and sample buffers hold those rows, in that order.
+ * ABI 2 added row_step (ipt_abi_version). */
 typedef struct ipt_params {
   int32_t width, height, spp, max_bounces;
   uint64_t seed;
   int32_t row_begin, row_end;
+  int32_t row_step;
 } ipt_params_t;
 
 const char *ipt_last_error(void);
 void ipt_clear_error(void);
-int ipt_abi_version(void);            /* 1 */
+int ipt_abi_version(void);            /* 2 */
 int ipt_device_count(void);
 /* Diagnostic: bitwise self-test of the kernels' in-range sqrt/division cores
  * against the IEEE operations over n random operands per test; counts[8]

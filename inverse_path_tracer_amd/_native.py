@@ -36,12 +36,20 @@ class Params(C.Structure):
         ("seed", C.c_uint64),
         ("row_begin", C.c_int32),
         ("row_end", C.c_int32),
+        ("row_step", C.c_int32),
     ]
 
+    @property
+    def rows(self) -> int:
+        """Image rows the launch traces (row_begin, row_begin + row_step, ... < row_end)."""
+        n = self.row_end - self.row_begin
+        return max(0, -(-n // max(1, self.row_step)))
 
-def make_params(width, height, spp, max_bounces=None, seed=0, row_begin=0, row_end=None) -> Params:
+
+def make_params(width, height, spp, max_bounces=None, seed=0, row_begin=0, row_end=None, row_step=1) -> Params:
     return Params(int(width), int(height), int(spp), -1 if max_bounces is None else int(max_bounces),
-                  int(seed) & 0xFFFFFFFFFFFFFFFF, int(row_begin), int(height if row_end is None else row_end))
+                  int(seed) & 0xFFFFFFFFFFFFFFFF, int(row_begin), int(height if row_end is None else row_end),
+                  int(row_step))
 
 
 _lib = None

@@ -34,6 +34,7 @@ ipt::RenderParams to_params(const ipt_params_t *p) {
   r.seed = p->seed;
   r.row_begin = p->row_begin;
   r.row_end = p->row_end;
+  r.row_step = p->row_step;
   return r;
 }
 
@@ -88,7 +89,7 @@ extern "C" {
 
 const char *ipt_last_error(void) { return g_err.c_str(); }
 void ipt_clear_error(void) { g_err.clear(); }
-int ipt_abi_version(void) { return 1; }
+int ipt_abi_version(void) { return 2; }
 int ipt_device_count(void) { return ipt::gpu_device_count(); }
 int ipt_selftest_math(uint64_t n, uint64_t seed, uint64_t *counts) {
   if (!counts) return -1;
@@ -325,7 +326,7 @@ void createGraph(void *scenePtr, char *imgFile, float *data) {
          std::to_string(p.width) + "x" + std::to_string(p.height));
     return;
   }
-  ipt_params_t q{p.width, p.height, p.spp, p.max_bounces, p.seed, 0, p.height};
+  ipt_params_t q{p.width, p.height, p.spp, p.max_bounces, p.seed, 0, p.height, 1};
   ipt_graph_host(scenePtr, &q, target.data(), nullptr, data);
 }
 

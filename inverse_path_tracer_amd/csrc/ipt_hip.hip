@@ -105,14 +105,15 @@ constexpr int kBvhLdsNodeBytes = IPT_BVH_LDS_KB * 1024;  // stage the whole tree
 struct TraceArgs {
   int W, H, spp, max_bounces;
   uint64_t seed;
-  uint64_t s_begin, n_samples;
+  uint64_t n_samples;
   int nT, nE;
   int lds_edges;  // GRAPH: bins privatised in LDS
   int sample_major;  // FWD: sample buffer [s][pixel][3] (else [pixel][s][3])
   int kd_tables;     // kd and kd/pi staged in LDS
   const float *kdpi_g;  // kd/pi in global memory (large scenes: no LDS tables), per launch
   int small_pairs;   // nT <= 2*kSmallPairs: unrolled closest-hit, plane offsets in LDS
-  uint64_t pix_begin, npix;
+  uint64_t npix;     // pixels of the launch (its rows x W)
+  int row0, row_step;  // traced rows: row0, row0 + row_step, ... (row_step 1: a contiguous band)
   // index arithmetic: when every global sample index of the frame is below
   // 2^32, g / spp and pixel / W use Lemire's multiply-high division
   // (M = ceil(2^64 / d), exact for 32-bit n and d > 1) instead of the ~40
@@ -155,19 +156,51 @@ struct TraceArgs {
 __device__ __forceinline__ uint32_t udiv32(uint32_t n, uint64_t m, uint32_t d) {
   return d == 1u ? n : (uint32_t)__umul64hi(m, (uint64_t)n);
 }
-// pixel index of global sample g
-__device__ __forceinline__ uint64_t sample_pixel(const TraceArgs &a, uint64_t g) {
-  return a.idx32 ? (uint64_t)udiv32((uint32_t)g, a.m_spp, (uint32_t)a.spp) : g / (uint64_t)a.spp;
+
+// Work item w of a launch -> (launch-local pixel lp, sample sj).  Pixel-major:
+// w = lp * spp + sj (a wave traces consecutive samples of one pixel).
+// Sample-major: w = sj * npix + lp (lane i of a wave writes slot base + i of a
+// [s][pixel][3] buffer -- one contiguous store run).
+__device__ __forceinline__ void item_split(const TraceArgs &a, uint64_t w, uint64_t &lp, uint64_t &sj) {
+  if (a.idx32) {
+    if (a.sample_major) {
+      const uint32_t q = udiv32((uint32_t)w, a.m_npix, (uint32_t)a.npix);
+      sj = q;
+      lp = (uint32_t)w - q * (uint32_t)a.npix;
+    } else {
+      const uint32_t q = udiv32((uint32_t)w, a.m_spp, (uint32_t)a.spp);
+      lp = q;
+      sj = (uint32_t)w - q * (uint32_t)a.spp;
+    }
+  } else if (a.sample_major) {
+    sj = w / a.npix;
+    lp = w - sj * a.npix;
+  } else {
+    lp = w / (uint64_t)a.spp;
+    sj = w - lp * (uint64_t)a.spp;
+  }
+}
+// launch-local pixel -> image row and column
+__device__ __forceinline__ void local_rc(const TraceArgs &a, uint64_t lp, int &r, int &c) {
+  uint64_t lr;
+  if (a.idx32) {
+    const uint32_t q = udiv32((uint32_t)lp, a.m_W, (uint32_t)a.W);
+    lr = q;
+    c = (int)((uint32_t)lp - q * (uint32_t)a.W);
+  } else {
+    lr = lp / (uint64_t)a.W;
+    c = (int)(lp - lr * (uint64_t)a.W);
+  }
+  r = a.row0 + (int)lr * a.row_step;
 }
 
-// pixel index of this launch's work item w (see the enumeration in trace_kernel)
+// global pixel index (r * W + c) of this launch's work item w
 __device__ __forceinline__ uint64_t item_pixel(const TraceArgs &a, uint64_t w) {
-  if (!a.sample_major) return sample_pixel(a, a.s_begin + w);
-  if (a.idx32) {
-    const uint32_t sj = udiv32((uint32_t)w, a.m_npix, (uint32_t)a.npix);
-    return (uint64_t)((uint32_t)a.pix_begin + ((uint32_t)w - sj * (uint32_t)a.npix));
-  }
-  return a.pix_begin + (w - (w / a.npix) * a.npix);
+  uint64_t lp, sj;
+  item_split(a, w, lp, sj);
+  int r, c;
+  local_rc(a, lp, r, c);
+  return (uint64_t)r * (uint64_t)a.W + (uint64_t)c;
 }
 
 using namespace dev;
@@ -177,32 +210,10 @@ using namespace dev;
 // enumeration is described in trace_kernel.
 __device__ __forceinline__ void item_ray(const TraceArgs &a, uint64_t seed, uint64_t w, Rng &st, V3 &p, V3 &d, int &r,
                                          int &c) {
-  uint64_t g;
-  if (a.idx32) {
-    uint32_t pixel;
-    if (a.sample_major) {
-      const uint32_t sj = udiv32((uint32_t)w, a.m_npix, (uint32_t)a.npix);
-      pixel = (uint32_t)a.pix_begin + ((uint32_t)w - sj * (uint32_t)a.npix);
-      g = (uint64_t)pixel * (uint32_t)a.spp + sj;
-    } else {
-      g = a.s_begin + w;
-      pixel = udiv32((uint32_t)g, a.m_spp, (uint32_t)a.spp);
-    }
-    r = (int)udiv32(pixel, a.m_W, (uint32_t)a.W);
-    c = (int)(pixel - (uint32_t)r * (uint32_t)a.W);
-  } else {
-    uint64_t pixel;
-    if (a.sample_major) {
-      const uint64_t sj = w / a.npix;
-      pixel = a.pix_begin + (w - sj * a.npix);
-      g = pixel * (uint64_t)a.spp + sj;
-    } else {
-      g = a.s_begin + w;
-      pixel = g / (uint64_t)a.spp;
-    }
-    r = (int)(pixel / (uint64_t)a.W);
-    c = (int)(pixel % (uint64_t)a.W);
-  }
+  uint64_t lp, sj;
+  item_split(a, w, lp, sj);
+  local_rc(a, lp, r, c);
+  const uint64_t g = ((uint64_t)r * (uint64_t)a.W + (uint64_t)c) * (uint64_t)a.spp + sj;  // global sample index
   rng_init(st, seed + g);
   camera_ray(a.cam, st, r, c, a.W, a.H, p, d);
 }
@@ -561,12 +572,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   // wave-uniform sample range (static partition, regenerated per lane)
   const uint32_t wave = __builtin_amdgcn_readfirstlane((sblock * kBlock + tid) >> 6);
   const uint32_t nwaves = (sgrid * kBlock) >> 6;
-  // Work items w in [0, n_samples) of this launch.  Pixel-major: w is sample
-  // g = s_begin + w (a wave traces consecutive samples of one pixel).
-  // Sample-major (FWD into a [s][pixel][3] buffer): w = s * npix + pixel, so
-  // lane i of a wave writes slot w = base + i -- one contiguous store run.
-  // Either way the sample's seed is seed + g: results do not depend on the
-  // enumeration.
+  // Work items w in [0, n_samples) of this launch (item_split): pixel-major
+  // w = lp * spp + s, or sample-major w = s * npix + lp over the launch's
+  // pixels lp.  Either way the sample's seed is seed + its global index g:
+  // results do not depend on the enumeration or on the row partition.
   uint64_t next = (a.n_samples * wave) / nwaves;
   const uint64_t end = (a.n_samples * (wave + 1)) / nwaves;
 
@@ -1389,8 +1398,8 @@ static int check_params(const GpuScene *s, const RenderParams &p) {
     return -1;
   }
   if (p.width <= 0 || p.height <= 0 || p.spp <= 0 || p.row_begin < 0 || p.row_end > p.height ||
-      p.row_begin > p.row_end) {
-    gpu_set_error("invalid render parameters (width/height/spp > 0, 0 <= row_begin <= row_end <= height)");
+      p.row_begin > p.row_end || p.row_step < 1) {
+    gpu_set_error("invalid render parameters (width/height/spp > 0, 0 <= row_begin <= row_end <= height, row_step >= 1)");
     return -1;
   }
   if ((uint64_t)p.width * (uint64_t)p.height * (uint64_t)p.spp >= (1ull << 40)) {
@@ -1447,8 +1456,8 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.spp = p.spp;
   a.max_bounces = p.max_bounces < 0 ? -1 : p.max_bounces;
   a.seed = p.seed;
-  a.s_begin = (uint64_t)p.row_begin * p.width * p.spp;
-  a.n_samples = (uint64_t)(p.row_end - p.row_begin) * p.width * p.spp;
+  const int rows = band_rows(p);
+  a.n_samples = (uint64_t)rows * p.width * p.spp;
   a.nT = s->host.nT;
   a.nE = s->host.nE;
   a.lds_edges = 0;
@@ -1456,8 +1465,9 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.kdpi_g = nullptr;
   a.kd_tables = s->host.nT <= kMaxTableTris ? 1 : 0;
   a.small_pairs = (IPT_PAIRS && IPT_SMALL_UNROLL && s->host.nT <= 2 * kSmallPairs) ? 1 : 0;
-  a.pix_begin = (uint64_t)p.row_begin * p.width;
-  a.npix = (uint64_t)(p.row_end - p.row_begin) * p.width;
+  a.npix = (uint64_t)rows * p.width;
+  a.row0 = p.row_begin;
+  a.row_step = p.row_step > 1 ? p.row_step : 1;
   const uint64_t total = (uint64_t)p.height * p.width * p.spp;
   a.idx32 = total <= 0xffffffffull ? 1 : 0;
   a.m_spp = p.spp > 1 ? ~0ull / (uint64_t)p.spp + 1 : 0;
@@ -1649,7 +1659,7 @@ int gpu_pixel_mean_sm(const float *samples_dev, int64_t npix, int spp, float *hd
 int gpu_render(GpuScene *s, const RenderParams &p, const float *kd_dev, float *hdr_dev, uint8_t *ldr_dev,
                void *stream) {
   if (check_params(s, p)) return -1;
-  const int64_t npix = (int64_t)(p.row_end - p.row_begin) * p.width;
+  const int64_t npix = (int64_t)band_rows(p) * p.width;
   const int sets = p.nscenes > 1 ? p.nscenes : 1;
   StreamScratch ws;
   if (ws.alloc((size_t)sets * npix * p.spp * 3 * sizeof(float), (hipStream_t)stream)) return -1;
@@ -1962,7 +1972,7 @@ struct DevBuf {
 
 int gpu_render_samples_host(GpuScene *s, const RenderParams &p, float *samples) {
   if (check_params(s, p)) return -1;
-  const size_t n = (size_t)(p.row_end - p.row_begin) * p.width * p.spp * 3;
+  const size_t n = (size_t)band_rows(p) * p.width * p.spp * 3;
   DevBuf b;
   HIP_TRY(hipMalloc(&b.p, std::max<size_t>(n, 1) * sizeof(float)));
   if (gpu_render_samples(s, p, nullptr, (float *)b.p, nullptr)) return -1;
@@ -1972,7 +1982,7 @@ int gpu_render_samples_host(GpuScene *s, const RenderParams &p, float *samples) 
 
 int gpu_render_host(GpuScene *s, const RenderParams &p, float *hdr, uint8_t *ldr) {
   if (check_params(s, p)) return -1;
-  const size_t npix = (size_t)(p.row_end - p.row_begin) * p.width;
+  const size_t npix = (size_t)band_rows(p) * p.width;
   DevBuf h, l;
   HIP_TRY(hipMalloc(&h.p, std::max<size_t>(npix, 1) * 3 * sizeof(float)));
   if (ldr) HIP_TRY(hipMalloc(&l.p, std::max<size_t>(npix, 1) * 3));

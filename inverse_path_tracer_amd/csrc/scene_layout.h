@@ -147,16 +147,26 @@ struct DevScene {
 
 // Explicit render parameters (the reference's compile-time constants,
 // scene.h:3-13, made run-time; defaults reproduce them).
+struct RenderParams;
+inline int band_rows(const RenderParams &p);
 struct RenderParams {
   int width, height, spp;
   int max_bounces;      // < 0: unbounded (reference semantics)
   uint64_t seed;
   int row_begin, row_end;
+  // rows row_begin, row_begin + row_step, ... < row_end are traced (1 =
+  // a contiguous band; world = the interleaved share of one rank)
+  int row_step = 1;
   // scene batch: nscenes material sets over this geometry in one launch,
   // set b with seed + b * seed_stride (kd, outputs, adjoint image, gradient
   // at per-set strides)
   int nscenes = 1;
   uint64_t seed_stride = 0;
 };
+// number of image rows a launch traces
+inline int band_rows(const RenderParams &p) {
+  const int n = p.row_end - p.row_begin;
+  return n <= 0 ? 0 : (p.row_step <= 1 ? n : (n + p.row_step - 1) / p.row_step);
+}
 
 }  // namespace ipt

@@ -6,8 +6,12 @@ data-path exchange because every sample's RNG is seeded by its GLOBAL index
 single-GPU result bit-for-bit (forward) or up to fp64 summation order
 (adjoint, graph).
 
-* Strong scaling (one image, C4): contiguous row bands per rank
-  (``shard_rows``); the forward needs no collective (``gather_rows`` only if a
+* Strong scaling (one image, C2 / C4): each rank traces a share of the rows.
+  ``shard_rows`` gives contiguous bands; ``shard_rows_interleaved`` gives rank
+  r the rows r, r + world, ... (row_step = world), which balances the cost:
+  at C4 the contiguous bands differ by 7.6% (max/mean: the light and the cube
+  sit in particular bands), interleaved shares by < 1% (bench.py
+  ``bands_*``).  The forward needs no collective (``gather_rows`` only if a
   rank wants the whole image); the adjoint's only exchange is ONE all-reduce
   of the nT*3 fp64 gradient (``allreduce_``), 720 B for 30 triangles --
   latency-bound on xGMI, no bucketing needed.
@@ -31,6 +35,12 @@ def shard_rows(height: int, world: int, rank: int):
     return begin, begin + base + (1 if rank < rem else 0)
 
 
+def shard_rows_interleaved(height: int, world: int, rank: int):
+    """(row_begin, row_end, row_step) of `rank`'s interleaved share: rows
+    rank, rank + world, ... < height (the C ABI's row_step)."""
+    return min(rank, height), height, max(1, world)
+
+
 def frame_seed(seed: int, frame: int, width: int, height: int, spp: int) -> int:
     """Seed of frame `frame`: its sample indices follow frame-1's (disjoint RNG streams)."""
     return (int(seed) + int(frame) * width * height * spp) & 0xFFFFFFFFFFFFFFFF
@@ -49,18 +59,24 @@ def allreduce_(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
-def gather_rows(band: torch.Tensor, height: int) -> torch.Tensor:
-    """All-gather row bands (shard_rows layout) into the full (H, W, C) image."""
+def gather_rows(band: torch.Tensor, height: int, interleaved: bool = False) -> torch.Tensor:
+    """All-gather the ranks' rows (shard_rows or shard_rows_interleaved
+    layout) into the full (H, W, C) image."""
     W, R = world()
     if W == 1:
         return band
-    bands = [shard_rows(height, W, r) for r in range(W)]
-    maxrows = max(e - b for b, e in bands)
-    pad = torch.zeros((maxrows,) + tuple(band.shape[1:]), dtype=band.dtype, device=band.device)
+    counts = [len(range(*shard_rows_interleaved(height, W, r))) if interleaved else
+              (lambda be: be[1] - be[0])(shard_rows(height, W, r)) for r in range(W)]
+    pad = torch.zeros((max(counts),) + tuple(band.shape[1:]), dtype=band.dtype, device=band.device)
     pad[: band.shape[0]] = band
     out = [torch.empty_like(pad) for _ in range(W)]
     dist.all_gather(out, pad)
-    return torch.cat([o[: e - b] for o, (b, e) in zip(out, bands)], dim=0)
+    if not interleaved:
+        return torch.cat([o[:n] for o, n in zip(out, counts)], dim=0)
+    full = torch.empty((height,) + tuple(band.shape[1:]), dtype=band.dtype, device=band.device)
+    for r, (o, n) in enumerate(zip(out, counts)):
+        full[r::W] = o[:n]
+    return full
 
 
 def graph_sharded(scene, target, width: int, height: int, spp: int, max_bounces=None, seed: int = 0,

@@ -202,34 +202,34 @@ class Scene:
         return t, idx
 
     # ---------------------------------------------------------- host-memory renders
-    def render_samples(self, width, height, spp, max_bounces=None, seed=0, row_begin=0, row_end=None):
-        p = N.make_params(width, height, spp, max_bounces, seed, row_begin, row_end)
-        out = np.zeros(((p.row_end - p.row_begin) * width * spp, 3), np.float32)
+    def render_samples(self, width, height, spp, max_bounces=None, seed=0, row_begin=0, row_end=None, row_step=1):
+        p = N.make_params(width, height, spp, max_bounces, seed, row_begin, row_end, row_step)
+        out = np.zeros((p.rows * width * spp, 3), np.float32)
         N.check(N.lib().ipt_render_samples_host(self.handle, C.byref(p), out.ctypes.data_as(N.fp)), "render_samples")
         return out
 
-    def render(self, width, height, spp, max_bounces=None, seed=0, row_begin=0, row_end=None, ldr=False):
+    def render(self, width, height, spp, max_bounces=None, seed=0, row_begin=0, row_end=None, ldr=False, row_step=1):
         """HDR image (rows, W, 3) = per-pixel mean of the samples (+ 8-bit tonemap)."""
-        p = N.make_params(width, height, spp, max_bounces, seed, row_begin, row_end)
-        rows = p.row_end - p.row_begin
+        p = N.make_params(width, height, spp, max_bounces, seed, row_begin, row_end, row_step)
+        rows = p.rows
         hdr = np.zeros((rows, width, 3), np.float32)
         u8 = np.zeros((rows, width, 3), np.uint8) if ldr else None
         N.check(N.lib().ipt_render_host(self.handle, C.byref(p), hdr.ctypes.data_as(N.fp),
                                         u8.ctypes.data_as(N.u8p) if ldr else None), "render")
         return (hdr, u8) if ldr else hdr
 
-    def adjoint(self, adj, width, height, spp, max_bounces, seed=0, row_begin=0, row_end=None):
+    def adjoint(self, adj, width, height, spp, max_bounces, seed=0, row_begin=0, row_end=None, row_step=1):
         """d(sum(adj * I))/dKd as (nT, 3) float64; adj is (H, W, 3)."""
-        p = N.make_params(width, height, spp, max_bounces, seed, row_begin, row_end)
+        p = N.make_params(width, height, spp, max_bounces, seed, row_begin, row_end, row_step)
         adj = np.ascontiguousarray(np.asarray(adj, np.float32).reshape(height, width, 3))
         g = np.zeros((self.nT, 3), np.float64)
         N.check(N.lib().ipt_adjoint_host(self.handle, C.byref(p), adj.ctypes.data_as(N.fp),
                                          g.ctypes.data_as(N.dp)), "adjoint")
         return g
 
-    def graph(self, target, width, height, spp, max_bounces=None, seed=0, row_begin=0, row_end=None):
+    def graph(self, target, width, height, spp, max_bounces=None, seed=0, row_begin=0, row_end=None, row_step=1):
         """createGraph: returns (acc[(nT+1)*nT, 8] float64, data[(nT+1)*nT*7] float32)."""
-        p = N.make_params(width, height, spp, max_bounces, seed, row_begin, row_end)
+        p = N.make_params(width, height, spp, max_bounces, seed, row_begin, row_end, row_step)
         target = np.ascontiguousarray(np.asarray(target, np.uint8).reshape(height, width, 3))
         acc = np.zeros(((self.nT + 1) * self.nT, N.ACC_WIDTH), np.float64)
         data = np.zeros((self.nT + 1) * self.nT * 7, np.float32)

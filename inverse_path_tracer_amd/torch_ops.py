@@ -37,8 +37,12 @@ def adjoint_into(scene: Scene, params: N.Params, kd: torch.Tensor, adj_full: tor
 
 
 def adjoint_band(scene: Scene, params: N.Params, kd, adj_band: torch.Tensor, grad: torch.Tensor):
-    """Adjoint for a row band whose adjoint image holds only rows [row_begin,row_end)."""
+    """Adjoint for a launch whose adjoint image holds only its own rows."""
     adj_band = adj_band.contiguous()
+    if params.row_step > 1:  # interleaved rows: scatter into a full-frame image
+        full = torch.zeros((params.height, params.width, 3), device=adj_band.device, dtype=torch.float32)
+        full[params.row_begin:params.row_end:params.row_step] = adj_band
+        return adjoint_into(scene, params, kd, full.data_ptr(), grad)
     base = adj_band.data_ptr() - params.row_begin * params.width * 3 * 4  # global-pixel indexing
     return adjoint_into(scene, params, kd, base, grad)
 
@@ -47,8 +51,7 @@ class _RenderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, kd, scene, params, adjoint_seed):
         kd_c = kd.detach().contiguous().float()
-        rows = params.row_end - params.row_begin
-        hdr = torch.empty((rows, params.width, 3), device=kd.device, dtype=torch.float32)
+        hdr = torch.empty((params.rows, params.width, 3), device=kd.device, dtype=torch.float32)
         render_into(scene, params, kd_c, hdr)
         ctx.scene, ctx.params, ctx.adjoint_seed = scene, params, adjoint_seed
         ctx.save_for_backward(kd_c)
@@ -70,12 +73,13 @@ def _replay_params(p: N.Params, adjoint_seed):
     if adjoint_seed is None:
         return p
     return N.Params(p.width, p.height, p.spp, p.max_bounces, int(adjoint_seed) & 0xFFFFFFFFFFFFFFFF, p.row_begin,
-                    p.row_end)
+                    p.row_end, p.row_step)
 
 
 def render(scene: Scene, kd: torch.Tensor, width: int, height: int, spp: int, max_bounces=4, seed: int = 0,
-           row_begin: int = 0, row_end=None, adjoint_seed=None) -> torch.Tensor:
-    """Differentiable render: HDR image of rows [row_begin, row_end) w.r.t. kd.
+           row_begin: int = 0, row_end=None, adjoint_seed=None, row_step: int = 1) -> torch.Tensor:
+    """Differentiable render: HDR image of rows row_begin, row_begin + row_step,
+    ... < row_end w.r.t. kd.
 
     The backward pass replays the forward's paths (adjoint_seed None) or
     traces the same configuration with seed `adjoint_seed`.  The second form
@@ -92,7 +96,7 @@ def render(scene: Scene, kd: torch.Tensor, width: int, height: int, spp: int, ma
     same-stream one, tests/test_gpu_full.py)."""
     if max_bounces is None and kd.requires_grad:
         raise ValueError("the adjoint needs a finite max_bounces (vertex records live in LDS)")
-    p = N.make_params(width, height, spp, max_bounces, seed, row_begin, row_end)
+    p = N.make_params(width, height, spp, max_bounces, seed, row_begin, row_end, row_step)
     return _RenderFn.apply(kd, scene, p, adjoint_seed)
 
 

@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared_functions():
         assert hasattr(L, name), name
         assert name in N.SIGNATURES, "python binding lacks %s" % name
-    assert L.ipt_abi_version() == 1
+    assert L.ipt_abi_version() == 2
 
 
 @pytest.mark.parametrize("soname", ["libpt.so", "libipt.so"])
@@ -128,3 +128,17 @@ def test_shard_rows_partition():
             assert all(b[1] == c[0] for b, c in zip(bands, bands[1:]))
             assert max(e - b for b, e in bands) - min(e - b for b, e in bands) <= 1
     assert frame_seed(0, 2, 512, 512, 64) == 2 * 512 * 512 * 64
+
+
+def test_interleaved_shares_partition_rows():
+    from inverse_path_tracer_amd import _native as N
+    from inverse_path_tracer_amd.distributed import shard_rows_interleaved
+
+    for H in (1, 7, 512, 1024, 1000):
+        for W in (1, 2, 3, 8, 13):
+            rows = []
+            for r in range(W):
+                b, e, s = shard_rows_interleaved(H, W, r)
+                rows += list(range(b, e, s))
+                assert N.make_params(16, H, 1, 2, 0, b, e, s).rows == len(range(b, e, s))
+            assert sorted(rows) == list(range(H))

@@ -121,12 +121,15 @@ def test_empty_band_and_bad_params(scenes):
 # ------------------------------------------------------------- sharding (C2/C4 sizes)
 @pytest.mark.parametrize("W,H,spp,mb,world", [(512, 512, 64, 4, 8), (1024, 1024, 32, 8, 8), (512, 512, 64, 4, 3)])
 def test_row_band_sharding_bit_exact(scenes, W, H, spp, mb, world):
-    from inverse_path_tracer_amd.distributed import shard_rows
+    from inverse_path_tracer_amd.distributed import shard_rows, shard_rows_interleaved
 
     P, _ = scenes["scene0"]
     full = P.render(W, H, spp, mb, 0)
     bands = [P.render(W, H, spp, mb, 0, *shard_rows(H, world, r)) for r in range(world)]
     assert np.array_equal(bits(np.concatenate(bands)), bits(full))
+    for r in range(world):  # interleaved shares (the bench's tile split)
+        b, e, st = shard_rows_interleaved(H, world, r)
+        assert np.array_equal(bits(P.render(W, H, spp, mb, 0, b, e, row_step=st)), bits(full[b:e:st]))
 
 
 # ------------------------------------------------------------- adjoint

@@ -129,6 +129,43 @@ def test_c4_band_adjoints_sum_to_full_and_match_oracle(scene0):
     np.testing.assert_allclose(parts[3], want, rtol=1e-9, atol=1e-12 * np.abs(want).max())
 
 
+def test_c4_interleaved_shares_equal_full_frame_and_sum_to_full_adjoint(scene0):
+    """The bench's tile split: rank r traces rows r, r+8, ... (row_step = 8)."""
+    P, _ = scene0
+    W, H = C4["W"], C4["H"]
+    a = (W, H, C4["spp"], C4["mb"], C4["seed"])
+    full = P.render(*a)
+    adj = np.random.RandomState(5).uniform(-1, 1, (H, W, 3)).astype(np.float32)
+    g_full = P.adjoint(adj, *a)
+    g = 0
+    for r in range(8):
+        share = P.render(*a, r, H, row_step=8)
+        assert share.shape == (128, W, 3)
+        assert np.array_equal(bits(share), bits(full[r::8])), r
+        g = g + P.adjoint(adj, *a, r, H, row_step=8)
+    np.testing.assert_allclose(g, g_full, rtol=1e-10, atol=1e-10 * np.abs(g_full).max())
+
+
+def test_interleaved_rows_through_autograd_match_oracle(scene0):
+    """torch_ops.render with row_step: forward rows == the oracle's, and the
+    backward (adjoint image scattered to global rows) == the oracle's adjoint
+    summed over those rows."""
+    from inverse_path_tracer_amd import torch_ops
+
+    P, Q = scene0
+    W, H, spp, mb, seed = 40, 37, 8, 4, 21
+    rows = list(range(2, H, 3))
+    kd = torch.tensor(P.materials, device="cuda", requires_grad=True)
+    img = torch_ops.render(P, kd, W, H, spp, mb, seed, 2, H, row_step=3)
+    assert img.shape == (len(rows), W, 3)
+    full, _, _ = Q.render(W, H, spp, mb, seed)
+    assert np.array_equal(bits(img.detach().cpu().numpy()), bits(full[rows]))
+    adj = np.random.RandomState(6).uniform(-1, 1, (H, W, 3)).astype(np.float32)
+    (img * torch.from_numpy(adj[rows]).cuda()).sum().backward()
+    want = sum(Q.adjoint(W, H, spp, mb, seed, adj, r, r + 1) for r in rows)
+    np.testing.assert_allclose(kd.grad.double().cpu().numpy(), want, rtol=1e-5, atol=1e-9)
+
+
 # ------------------------------------------------------------- C5 scene batch
 def test_scene_batch_equals_single_launches(scene0, oracle):
     """ipt_render_batch_dev / ipt_adjoint_batch_dev: set b == the single-scene
