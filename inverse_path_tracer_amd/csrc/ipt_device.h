@@ -536,11 +536,16 @@ struct BvhView {
 };
 constexpr int kStackStride = 256;  // = the megakernel's block size
 constexpr int kBvhDone = (int)0x80000000;
-// Profiling build (make variant DEFS=-DIPT_BVH_STATS): casts, inner-node
-// visits, leaf pair tests and shadow early-outs, summed over all lanes
-// (ipt_debug_bvh_stats) -- the "tests actually executed" of the roofline.
+// Profiling build (make variant DEFS=-DIPT_BVH_STATS): work counters summed
+// over all lanes (ipt_debug_bvh_stats) -- the "tests actually executed" of
+// the roofline.  Cooperative traversal: [0] tree rays, [1] 8-wide node
+// visits, [2] leaf visits, [3] shadow rays occluded in the tree, [4] leaf
+// triangle tests, [5] coop calls with >= 1 ray (per wave), [6] coop rounds
+// (per wave); pre-pass: [7] casts, [8] large-triangle tests, [9] shadow
+// target tests, [10] shadow rays decided before the tree.
+constexpr int kBvhStats = 12;
 #ifdef IPT_BVH_STATS
-__device__ unsigned long long g_bvh_stats[4];
+__device__ unsigned long long g_bvh_stats[kBvhStats];
 #endif
 
 __device__ __forceinline__ void bvh_load_node(const BvhView &B, int n, float4 &q0, float4 &q1, float4 &q2,
@@ -667,13 +672,28 @@ __device__ __forceinline__ bool bvh_prepass(const BvhView &B, V3 p, V3 d, float 
     bi = target;
   } else
 #endif
+#ifdef IPT_BVH_STATS
+  atomicAdd(&g_bvh_stats[7], 1ull);
+  atomicAdd(&g_bvh_stats[8], 2ull * (unsigned long long)B.nbig);
+  if (SHADOW) atomicAdd(&g_bvh_stats[9], 1ull);
+#endif
   if (SHADOW) {
     hit_test(B.isect[target], target, p, d, bt, bi);
-    if (bi < 0) return false;  // the target itself is missed: not the closest hit either
+    if (bi < 0) {  // the target itself is missed: not the closest hit either
+#ifdef IPT_BVH_STATS
+      atomicAdd(&g_bvh_stats[10], 1ull);
+#endif
+      return false;
+    }
   }
   if (B.nbig > 0) {
     bvh_big_pass<SHADOW>(B, p, d, bt, bi);
-    if (SHADOW && bi != target) return false;  // occluded by a large triangle: decided
+    if (SHADOW && bi != target) {  // occluded by a large triangle: decided
+#ifdef IPT_BVH_STATS
+      atomicAdd(&g_bvh_stats[10], 1ull);
+#endif
+      return false;
+    }
   }
   return true;
 }
@@ -835,7 +855,13 @@ __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3
   const int lane = (int)__lane_id();
   const int g = lane >> 3, j = lane & 7;
   uint64_t M = __ballot(need);
+#ifdef IPT_BVH_STATS
+  if (M && lane == (int)__builtin_ctzll(__ballot(1))) atomicAdd(&g_bvh_stats[5], 1ull);
+#endif
   while (M) {
+#ifdef IPT_BVH_STATS
+    if (lane == (int)__builtin_ctzll(__ballot(1))) atomicAdd(&g_bvh_stats[6], 1ull);
+#endif
     uint64_t Mr = M;  // the first (up to) 8 rays: group k takes the k-th
     int src = -1;
 #pragma unroll
@@ -904,6 +930,9 @@ __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3
 #endif
           const int code = ~node;
           const int first = code >> 4, cnt = (code & 15) + 1;
+#ifdef IPT_BVH_STATS
+          if (j == 0) atomicAdd(&g_bvh_stats[4], (unsigned long long)cnt);
+#endif
           for (int base = 0; base < cnt; base += 8) {
             float tj = __builtin_inff();
             int ij = 0x7fffffff;

@@ -1280,9 +1280,10 @@ extern "C" int ipt_debug_phase_cycles(unsigned long long *out) {  // read and re
 #endif
 
 #ifdef IPT_BVH_STATS
-extern "C" int ipt_debug_bvh_stats(unsigned long long *out) {  // read and reset (4 counters)
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bvh_stats), 4 * sizeof(unsigned long long)) != hipSuccess) return -1;
-  unsigned long long z[4] = {0, 0, 0, 0};
+extern "C" int ipt_debug_bvh_stats(unsigned long long *out) {  // read and reset (kBvhStats counters)
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bvh_stats), kBvhStats * sizeof(unsigned long long)) != hipSuccess)
+    return -1;
+  unsigned long long z[kBvhStats] = {0};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_bvh_stats), z, sizeof z) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -19,6 +19,9 @@ CUBE_KD = "*Kd 0.9041462985304743 0.5854651848798454 0.007022117649276849*"  # s
 # object records (pos, ori, scl, obj, mtl) -- the oracle's and the product's input
 CORNELL = [((0, 0, 4), (0, 0, 0), (2, 2, 2), CORNELL_OBJ, CORNELL_MTL)]
 SCENE0 = CORNELL + [((0, -1.5, 4), (0, 0, 0), (1, 1, 1), CUBE_OBJ, CUBE_KD)]
+# BASELINE.json configs[2] as the north_star names it: "CornellBox + shapes/sphere.obj + cube.obj" --
+# scenes/0.txt plus a sphere (assets/northstar.txt; no shipped scene file uses sphere.obj), 1310 triangles
+NORTHSTAR = SCENE0 + [((-1.2, -1.35, 4.6), (0, 0, 0), (1.2, 1.2, 1.2), SPHERE_OBJ, "*Kd 0.2 0.6 0.3*")]
 
 
 def pytest_configure(config):

@@ -34,6 +34,9 @@ SCENES = {
     "scene0": [CORNELL, CUBE0],
     "sphere": [CORNELL, SPHERE],
     "clutter": [CORNELL, SPHERE, CUBE2, SPHERE2],
+    # BASELINE configs[2] as the north_star names it (assets/northstar.txt): 1310 triangles
+    "northstar": [CORNELL, CUBE0, (os.path.join(A, "shapes", "sphere.obj"), "*Kd 0.2 0.6 0.3*", (-1.2, -1.35, 4.6),
+                                   (0.0, 0.0, 0.0), (1.2, 1.2, 1.2))],
 }
 
 

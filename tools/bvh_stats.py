@@ -1,12 +1,16 @@
 """BVH work counters of a profiling build (make variant V=stats
-DEFS=-DIPT_BVH_STATS): per cast, inner-node visits and leaf pair tests,
-and the shadow early-out rate, on the forward of a large scene.
+DEFS=-DIPT_BVH_STATS) over the forward and the adjoint of large scenes at the
+C2/C3 size: the "tests actually executed" that the roofline of a BVH scene
+charges.
 
-    IPT_AMD_LIB=inverse_path_tracer_amd/lib/variants/libipt_stats.so \
-        python tools/bvh_stats.py [--scene sphere] [--size 512] [--spp 64]
+    IPT_AMD_LIB=inverse_path_tracer_amd/lib/variants/libipt_stats.so \\
+        python tools/bvh_stats.py [--scenes northstar,sphere] [--size 512] [--spp 64]
 
-Prints one JSON line: the "tests actually executed" that the roofline of a
-BVH scene charges.
+Writes profiles/bvh_stats.json: per scene and integrator the raw counters
+(ipt_device.h kBvhStats) and per sample: triangle tests (large-triangle
+pre-pass + shadow target + leaf), box tests (root + 8 per 8-wide node visit),
+and the algorithmic FLOP per sample = 38 * triangle tests + 12 * box tests
+(a slab test is 6 FMA; its min/max are not counted).
 """
 import argparse
 import ctypes as C
@@ -24,34 +28,61 @@ from bench_scenes import SCENES  # noqa: E402
 from inverse_path_tracer_amd import _native as N  # noqa: E402
 from inverse_path_tracer_amd.scene import ObjectSpec, Scene  # noqa: E402
 
+NAMES = ["tree_rays", "node_visits", "leaf_visits", "shadow_occluded_in_tree", "leaf_tri_tests", "coop_calls",
+         "coop_rounds", "casts", "prepass_tri_tests", "shadow_target_tests", "shadow_decided_before_tree", "unused"]
+
+
+def derive(c, n):
+    tri = c["prepass_tri_tests"] + c["shadow_target_tests"] + c["leaf_tri_tests"]
+    roots = c["casts"] - c["shadow_decided_before_tree"]
+    box = roots + 8 * c["node_visits"]
+    return {"samples": n, "casts_per_sample": c["casts"] / n, "tri_tests_per_sample": tri / n,
+            "box_tests_per_sample": box / n, "flop_per_sample": (38 * tri + 12 * box) / n,
+            "tree_rays_per_cast": c["tree_rays"] / max(1, c["casts"]),
+            "nodes_per_tree_ray": c["node_visits"] / max(1, c["tree_rays"]),
+            "leaf_tris_per_tree_ray": c["leaf_tri_tests"] / max(1, c["tree_rays"]),
+            "rays_per_coop_round": c["tree_rays"] / max(1, c["coop_rounds"]),
+            "rounds_per_coop_call": c["coop_rounds"] / max(1, c["coop_calls"])}
+
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--scene", default="sphere")
+    ap.add_argument("--scenes", default="northstar,sphere")
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--bounces", type=int, default=4)
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "bvh_stats.json"))
     args = ap.parse_args()
     L = N.lib()
     stats = L.ipt_debug_bvh_stats
     stats.argtypes = [C.POINTER(C.c_ulonglong)]
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    scene = Scene([ObjectSpec(o, m, p, r, s) for (o, m, p, r, s) in SCENES[args.scene]])
     W = H = args.size
-    samples = torch.empty((W * H * args.spp, 3), device=dev)
-    p = N.make_params(W, H, args.spp, args.bounces, 0)
-    buf = (C.c_ulonglong * 4)()
-    stats(buf)  # reset
-    N.check(L.ipt_render_samples_sm_dev(scene.handle, C.byref(p), None, samples.data_ptr(), None))
-    torch.cuda.synchronize()
-    stats(buf)
-    casts, nodes, pairs, occluded = list(buf)
     n = W * H * args.spp
-    print(json.dumps({"scene": args.scene, "triangles": scene.nT, "samples": n, "casts": casts,
-                      "casts_per_sample": casts / n, "nodes_per_cast": nodes / casts,
-                      "pair_tests_per_cast": pairs / casts, "tri_tests_per_cast": 2 * pairs / casts,
-                      "shadow_early_out": occluded, "bvh": scene.bvh_info()}), flush=True)
+    samples = torch.empty((n, 3), device=dev)
+    adj = torch.ones((H, W, 3), device=dev)
+    buf = (C.c_ulonglong * len(NAMES))()
+    out = {}
+    for name in args.scenes.split(","):
+        scene = Scene([ObjectSpec(o, m, p, r, s) for (o, m, p, r, s) in SCENES[name]])
+        grad = torch.zeros((scene.nT, 3), device=dev, dtype=torch.float64)
+        p = N.make_params(W, H, args.spp, args.bounces, 0)
+        for kind in ("fwd", "adj"):
+            stats(buf)  # reset
+            if kind == "fwd":
+                N.check(L.ipt_render_samples_sm_dev(scene.handle, C.byref(p), None, samples.data_ptr(), None))
+            else:
+                N.check(L.ipt_adjoint_dev(scene.handle, C.byref(p), None, adj.data_ptr(), grad.data_ptr(), None))
+            torch.cuda.synchronize()
+            stats(buf)
+            c = dict(zip(NAMES, list(buf)))
+            out["%s_%s" % (name, kind)] = {"triangles": scene.nT, "config": [W, H, args.spp, args.bounces, 0],
+                                           "counters": c, "derived": derive(c, n), "bvh": scene.bvh_info()}
+            print(name, kind, json.dumps(out["%s_%s" % (name, kind)]["derived"]), flush=True)
+        scene.close()
+    with open(args.out, "w") as f:
+        json.dump(out, f, indent=1)
 
 
 if __name__ == "__main__":

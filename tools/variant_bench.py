@@ -28,6 +28,9 @@ if os.environ.get("IPT_VB_CLUTTER"):  # the 4-object scene of tests/test_bvh.py 
         (A + "/shapes/sphere.obj", "*Kd 0.2 0.6 0.3*", (0.3, -1.2, 4.2), (0.0, 0.4, 0.0), (1.2, 1.2, 1.2)),
         (A + "/shapes/cube.obj", "*Kd 0.5 0.5 0.5*", (-0.9, -1.4, 3.9), (0.2, 0.7, 0.1), (0.7, 0.7, 0.7)),
         (A + "/shapes/sphere.obj", "*Kd 0.9 0.1 0.1*", (0.8, 0.9, 4.6), (0.0, 0.0, 0.5), (0.5, 0.5, 0.5))]
+if os.environ.get("IPT_VB_NORTHSTAR"):  # BASELINE configs[2]: scenes/0.txt + sphere (1310 triangles)
+    SCENES["northstar"] = SCENES["scene0"] + [(A + "/shapes/sphere.obj", "*Kd 0.2 0.6 0.3*", (-1.2, -1.35, 4.6),
+                                               (0.0, 0.0, 0.0), (1.2, 1.2, 1.2))]
 if os.environ.get("IPT_VB_ONLY"):  # comma-separated scene names
     SCENES = {k: v for k, v in SCENES.items() if k in os.environ["IPT_VB_ONLY"].split(",")}
 
