@@ -431,12 +431,12 @@ __device__ __forceinline__ void pair_ray(const TriPair &T, const PairOrigin &o, 
   if (LEX) {
     const bool va = !(fabsf(denom.x) < kMinDotUp) && !(t.x < kEpsUp) && !(s0.x > 0.f) && !(s1.x > 0.f) &&
                     !(s2.x > 0.f);
-    const bool ta = va && (t.x < bt || (t.x == bt && ia < bi));
+    const bool ta = va & ((t.x < bt) | ((t.x == bt) & (ia < bi)));  // bitwise: no exec-mask branches
     bt = ta ? t.x : bt;
     bi = ta ? ia : bi;
     const bool vb = !(fabsf(denom.y) < kMinDotUp) && !(t.y < kEpsUp) && !(s0.y > 0.f) && !(s1.y > 0.f) &&
                     !(s2.y > 0.f);
-    const bool tb = vb && (t.y < bt || (t.y == bt && ib < bi));
+    const bool tb = vb & ((t.y < bt) | ((t.y == bt) & (ib < bi)));
     bt = tb ? t.y : bt;
     bi = tb ? ib : bi;
     return;
@@ -589,11 +589,11 @@ __device__ __forceinline__ void bvh_pair_test(const BvhPair &T, V3 p, V3 d, floa
   const f2 s2 = fma2(qz, f2{T.f[16][0], T.f[16][1]}, fma2(qy, f2{T.f[15][0], T.f[15][1]},
                                                           fma2(qx, f2{T.f[14][0], T.f[14][1]}, f2{T.f[17][0], T.f[17][1]})));
   const bool va = !(fabsf(denom.x) < kMinDotUp) && !(t.x < kEpsUp) && !(s0.x > 0.f) && !(s1.x > 0.f) && !(s2.x > 0.f);
-  const bool ta = va && (t.x < bt || (t.x == bt && T.idx[0] < bi));
+  const bool ta = va & ((t.x < bt) | ((t.x == bt) & (T.idx[0] < bi)));
   bt = ta ? t.x : bt;
   bi = ta ? T.idx[0] : bi;
   const bool vb = !(fabsf(denom.y) < kMinDotUp) && !(t.y < kEpsUp) && !(s0.y > 0.f) && !(s1.y > 0.f) && !(s2.y > 0.f);
-  const bool tb = vb && (t.y < bt || (t.y == bt && T.idx[1] < bi));
+  const bool tb = vb & ((t.y < bt) | ((t.y == bt) & (T.idx[1] < bi)));
   bt = tb ? t.y : bt;
   bi = tb ? T.idx[1] : bi;
 }
@@ -604,6 +604,19 @@ __device__ __forceinline__ void bvh_pair_test(const BvhPair &T, V3 p, V3 d, floa
 // in ascending original index, so the strict in-order accept is then already
 // the lexicographic minimum (2-3 fewer VALU per triangle); the shadow
 // pre-pass starts from the target's (t, index) and needs LEX.
+// The pairs and indices are read through the constant address space: the
+// kernel writes global memory, so through a plain pointer (reached via the
+// TraceArgs kernarg, not a __restrict__ parameter) the compiler may not use
+// the scalar cache and emits per-lane vector loads of the same 144 B.
+typedef __attribute__((address_space(4))) const float cst_f32;
+typedef __attribute__((address_space(4))) const int32_t cst_i32;
+__device__ __forceinline__ TriPair load_pair_cst(const TriPair *p) {
+  const cst_f32 *q = (const cst_f32 *)p;
+  TriPair T;
+#pragma unroll
+  for (int i = 0; i < 36; ++i) T.f[i >> 1][i & 1] = q[i];
+  return T;
+}
 template <bool LEX>
 __device__ __forceinline__ void bvh_big_pass(const BvhView &B, V3 p, V3 d, float &bt, int &bi) {
   int nP = B.nbig;
@@ -611,12 +624,13 @@ __device__ __forceinline__ void bvh_big_pass(const BvhView &B, V3 p, V3 d, float
   typedef __attribute__((address_space(3))) const f2 lds_f2;  // LDS base pinned in a VGPR (see closest_hit_pairs_small)
   lds_f2 *e3l = (lds_f2 *)B.big_e3;
   if (IPT_PIN_E3) asm volatile("" : "+v"(e3l));
+  const cst_i32 *bidx = (const cst_i32 *)B.big_idx;
 #pragma unroll
   for (int j = 0; j < kSmallPairs; ++j) {
     if (j < nP) {  // wave-uniform
-      const TriPair T = B.big[j];
-      pair_ray<LEX>(T, pair_origin(T, p), B.big_idx[2 * j], B.big_idx[2 * j + 1], p, d, bt, bi, e3l[3 * j],
-                    e3l[3 * j + 1], e3l[3 * j + 2]);
+      const TriPair T = load_pair_cst(B.big + j);
+      pair_ray<LEX>(T, pair_origin(T, p), bidx[2 * j], bidx[2 * j + 1], p, d, bt, bi, e3l[3 * j], e3l[3 * j + 1],
+                    e3l[3 * j + 2]);
     }
   }
 }
@@ -803,7 +817,7 @@ template <int CTRL>
 __device__ __forceinline__ void lexmin_dpp(float &t, int &i) {
   const float t2 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(t), CTRL, 0xf, 0xf, false));
   const int i2 = __builtin_amdgcn_update_dpp(0, i, CTRL, 0xf, 0xf, false);
-  const bool take = t2 < t || (t2 == t && i2 < i);
+  const bool take = (t2 < t) | ((t2 == t) & (i2 < i));
   t = take ? t2 : t;
   i = take ? i2 : i;
 }
@@ -942,10 +956,9 @@ __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3
               ij = __float_as_int(T.pad[0]);
             }
             group_lexmin(tj, ij);
-            if (tj < gt || (tj == gt && ij < gi)) {
-              gt = tj;
-              gi = ij;
-            }
+            const bool take = (tj < gt) | ((tj == gt) & (ij < gi));
+            gt = take ? tj : gt;
+            gi = take ? ij : gi;
           }
           node = (SHADOW && gi != target) ? kBvhDone : (sp > 0 ? (int)stk[--sp] : kBvhDone);
         }
