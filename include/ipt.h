@@ -123,6 +123,11 @@ int ipt_scene_bvh_info(void *scene, int32_t *info8);
  * info8[4]*2 int32 (the pre-pass triangles, 0x7fffffff = padding); each
  * nullable. */
 int ipt_scene_export_bvh(void *scene, float *nodes, float *pairs, int32_t *big_idx);
+/* The 8-wide nodes of the cooperative traversal (info8[5] of them): wide
+ * receives info8[5]*64 floats (WideNode: per child lo.xyz, hi.xyz, ref bits,
+ * pad), qwide info8[5]*36 uint32 (QWideNode: origin xyz float bits, step
+ * exponent bytes, per child packed 8-bit bounds, ref, 0); each nullable. */
+int ipt_scene_export_wide(void *scene, float *wide, uint32_t *qwide);
 /* Closest hit of n rays (origins, dirs: n*3 floats) through the kernels'
  * own cast: idx = triangle index or -1, t = its distance.  targets
  * (nullable, n ints): >= 0 marks a next-event shadow ray towards that

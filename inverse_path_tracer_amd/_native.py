@@ -103,6 +103,7 @@ SIGNATURES = {
     "ipt_scene_set_accel": (C.c_int, [vp, C.c_int]),
     "ipt_scene_bvh_info": (C.c_int, [vp, C.POINTER(C.c_int32)]),
     "ipt_scene_export_bvh": (C.c_int, [vp, fp, fp, C.POINTER(C.c_int32)]),
+    "ipt_scene_export_wide": (C.c_int, [vp, fp, C.POINTER(C.c_uint32)]),
     "ipt_closest_hit_host": (C.c_int, [vp, C.c_int64, fp, fp, C.POINTER(C.c_int32), fp, C.POINTER(C.c_int32)]),
     "ipt_closest_hit_dev": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp, vp, vp]),
     "ipt_png_write": (C.c_int, [C.c_char_p, C.c_int, C.c_int, u8p]),

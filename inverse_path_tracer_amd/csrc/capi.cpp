@@ -214,6 +214,15 @@ int ipt_scene_export_bvh(void *scene, float *nodes, float *pairs, int32_t *big_i
   if (pairs && !h.bvh_pairs.empty()) std::memcpy(pairs, h.bvh_pairs.data(), h.bvh_pairs.size() * sizeof(ipt::BvhPair));
   return 0;
 }
+int ipt_scene_export_wide(void *scene, float *wide, uint32_t *qwide) {
+  GpuScene *s = as_scene(scene);
+  if (!s) return -1;
+  const ipt::HostScene &h = ipt::gpu_host(s);
+  if (wide && !h.bvh_wide.empty()) std::memcpy(wide, h.bvh_wide.data(), h.bvh_wide.size() * sizeof(ipt::WideNode));
+  if (qwide && !h.bvh_qwide.empty())
+    std::memcpy(qwide, h.bvh_qwide.data(), h.bvh_qwide.size() * sizeof(ipt::QWideNode));
+  return 0;
+}
 int ipt_scene_set_accel(void *scene, int mode) {
   GpuScene *s = as_scene(scene);
   if (!s) return -1;

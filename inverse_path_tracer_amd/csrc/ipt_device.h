@@ -804,8 +804,15 @@ __device__ __forceinline__ int closest_hit_bvh(const BvhView &B, V3 p, V3 d, flo
 // All lanes of a group hold identical copies of the ray state, so every
 // branch is group-uniform and the DPP reductions (xor 1, xor 2 within quads,
 // half-row mirror) only read lanes of the same, active group.
+// IPT_BVH_QNODES=1 (default): the traversal reads QWideNode (144 B, 9
+// float4) instead of WideNode (256 B, 16 float4): the northstar tree (143
+// nodes) fits the LDS stage; decoding costs ~18 VALU per lane and visit.
+#ifndef IPT_BVH_QNODES
+#define IPT_BVH_QNODES 1
+#endif
+constexpr int kWideF4 = IPT_BVH_QNODES ? 9 : 16;  // float4 per wide node
 struct CoopView {
-  const float4 *wn;    // wide nodes: slot j of node n at wn[2 * (8 * n + j) + {0, 1}]
+  const float4 *wn;    // wide nodes (WideNode or QWideNode, kWideF4 float4 each)
   bool wn_lds;         // wn points into LDS (else global memory)
   const TriIsect *wt;  // leaf triangles, pad[0] = original index
   uint32_t *stk;       // LDS: this wave's 8 group stacks, `stride` entries each
@@ -906,6 +913,28 @@ __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3
 #ifdef IPT_BVH_STATS
           ++st_nodes;
 #endif
+#if IPT_BVH_QNODES
+          // QWideNode: header (grid origin, step exponents) + this lane's child
+          v4f hd, ch;
+          if (C.wn_lds) {  // typed per branch: ds_read_b128, not a flat load
+            const lds_v4 *q = (const lds_v4 *)C.wn + kWideF4 * node;
+            hd = q[0];
+            ch = q[1 + j];
+          } else {
+            const gbl_v4 *q = (const gbl_v4 *)C.wn + kWideF4 * node;
+            hd = q[0];
+            ch = q[1 + j];
+          }
+          const uint32_t eb = __float_as_uint(hd.w);
+          const float sx = __uint_as_float((eb & 0xffu) << 23), sy = __uint_as_float(((eb >> 8) & 0xffu) << 23);
+          const float sz = __uint_as_float(((eb >> 16) & 0xffu) << 23);
+          const uint32_t w0 = __float_as_uint(ch.x), w1 = __float_as_uint(ch.y);
+          // o + q * 2^e: exact (scene_layout.h), so these are the grid boxes themselves
+          const float4 a = make_float4(fmaf((float)(w0 & 0xffu), sx, hd.x), fmaf((float)((w0 >> 8) & 0xffu), sy, hd.y),
+                                       fmaf((float)((w0 >> 16) & 0xffu), sz, hd.z), fmaf((float)(w0 >> 24), sx, hd.x));
+          const float4 b = make_float4(fmaf((float)(w1 & 0xffu), sy, hd.y), fmaf((float)((w1 >> 8) & 0xffu), sz, hd.z),
+                                       ch.z, 0.f);
+#else
           float4 a, b;
           if (C.wn_lds) {  // typed per branch: ds_read_b128, not a flat load
             const lds_v4 *q = (const lds_v4 *)C.wn + 2 * (8 * node + j);
@@ -918,6 +947,7 @@ __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3
             a = make_float4(qa.x, qa.y, qa.z, qa.w);
             b = make_float4(qb.x, qb.y, qb.z, qb.w);
           }
+#endif
           const int ref = __float_as_int(b.z);
           const float tx0 = fmaf(a.x, r.ix.x, r.ox.x), tx1 = fmaf(a.w, r.ix.x, r.ox.x);
           const float ty0 = fmaf(a.y, r.iy.x, r.oy.x), ty1 = fmaf(b.x, r.iy.x, r.oy.x);

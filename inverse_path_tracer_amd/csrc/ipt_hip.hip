@@ -126,7 +126,7 @@ struct TraceArgs {
   int bvh_nbig;                 // large-triangle pairs tested before the traversal
   // cooperative traversal (IPT_BVH_COOP): 8-wide nodes (first bvh_wide_lds of
   // them staged in LDS: all or none), leaf triangles, group-stack entries
-  const WideNode *bvh_wide;
+  const float4 *bvh_wide;  // WideNode or QWideNode records (kWideF4 float4 each)
   const TriIsect *bvh_wtris;
   int bvh_wide_lds, coop_stride;
   float root_box[6];
@@ -200,6 +200,7 @@ __device__ __forceinline__ uint64_t item_pixel(const TraceArgs &a, uint64_t w) {
   item_split(a, w, lp, sj);
   int r, c;
   local_rc(a, lp, r, c);
+  if (a.idx32) return (uint32_t)r * (uint32_t)a.W + (uint32_t)c;
   return (uint64_t)r * (uint64_t)a.W + (uint64_t)c;
 }
 
@@ -213,7 +214,13 @@ __device__ __forceinline__ void item_ray(const TraceArgs &a, uint64_t seed, uint
   uint64_t lp, sj;
   item_split(a, w, lp, sj);
   local_rc(a, lp, r, c);
-  const uint64_t g = ((uint64_t)r * (uint64_t)a.W + (uint64_t)c) * (uint64_t)a.spp + sj;  // global sample index
+  uint64_t g;  // global sample index
+  if (a.idx32) {  // every index of the frame fits 32 bits: one 32x32->64 multiply-add
+    const uint32_t pixel = (uint32_t)r * (uint32_t)a.W + (uint32_t)c;
+    g = (uint64_t)pixel * (uint32_t)a.spp + sj;
+  } else {
+    g = ((uint64_t)r * (uint64_t)a.W + (uint64_t)c) * (uint64_t)a.spp + sj;
+  }
   rng_init(st, seed + g);
   camera_ray(a.cam, st, r, c, a.W, a.H, p, d);
 }
@@ -523,14 +530,13 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       bv.lnodes = ln;
     }
     float4 *lw = ln + 4 * a.bvh_lds_nodes;
-    cv.wn = reinterpret_cast<const float4 *>(a.bvh_wide);
+    cv.wn = a.bvh_wide;
     if (kCoop && a.bvh_wide_lds > 0) {
-      const float4 *g = reinterpret_cast<const float4 *>(a.bvh_wide);
-      for (int i = tid; i < 16 * a.bvh_wide_lds; i += nthr) lw[i] = g[i];
+      for (int i = tid; i < kWideF4 * a.bvh_wide_lds; i += nthr) lw[i] = a.bvh_wide[i];
       cv.wn = lw;
       cv.wn_lds = true;
     }
-    float *be3 = reinterpret_cast<float *>(lw + 16 * a.bvh_wide_lds);
+    float *be3 = reinterpret_cast<float *>(lw + kWideF4 * a.bvh_wide_lds);
     for (int i = tid; i < 6 * a.bvh_nbig; i += nthr) {
       const int j = i / 6, kf = (i % 6) >> 1, h = i & 1;
       be3[i] = a.bvh_big[j].f[9 + 4 * kf][h];
@@ -1263,7 +1269,7 @@ struct GpuScene {
   BvhPair *bpairs = nullptr;
   TriPair *big_pairs = nullptr;
   int32_t *big_idx = nullptr;
-  WideNode *wide = nullptr;
+  float4 *wide = nullptr;  // WideNode or QWideNode records (IPT_BVH_QNODES)
   TriIsect *wtris = nullptr;
   int accel = IPT_ACCEL_AUTO;
   int *grad_map = nullptr, *slot_tri = nullptr;  // ADJ hot-set LDS slots (large scenes)
@@ -1299,6 +1305,14 @@ static int upload(T **dst, const std::vector<T> &v) {
   return 0;
 }
 
+template <typename T>
+static int upload_as_f4(float4 **dst, const std::vector<T> &v) {
+  static_assert(sizeof(T) % sizeof(float4) == 0, "record is not a whole number of float4");
+  HIP_TRY(hipMalloc(reinterpret_cast<void **>(dst), std::max<size_t>(v.size(), 1) * sizeof(T)));
+  if (!v.empty()) HIP_TRY(hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return 0;
+}
+
 GpuScene *gpu_upload(const HostScene &host, std::string *err) {
   GpuScene *s = new GpuScene();
   s->host = host;
@@ -1313,7 +1327,8 @@ GpuScene *gpu_upload(const HostScene &host, std::string *err) {
       upload(&s->kd, host.kd) || upload(&s->emit_tri, host.emit_tri) || upload(&s->emit_cdf, host.emit_cdf) ||
       upload(&s->emit_pmf, host.emit_pmf) || upload(&s->bnodes, host.bvh_nodes) || upload(&s->bpairs, host.bvh_pairs) ||
       upload(&s->big_pairs, host.bvh_big_pairs) || upload(&s->big_idx, host.bvh_big_idx) ||
-      upload(&s->wide, host.bvh_wide) || upload(&s->wtris, host.bvh_wtris)) {
+      (IPT_BVH_QNODES ? upload_as_f4(&s->wide, host.bvh_qwide) : upload_as_f4(&s->wide, host.bvh_wide)) ||
+      upload(&s->wtris, host.bvh_wtris)) {
     *err = gpu_last_error();
     gpu_free(s);
     return nullptr;
@@ -1516,14 +1531,14 @@ static size_t bvh_lds(const GpuScene *s, TraceArgs &a, size_t base, bool server)
   const size_t nw = s->host.bvh_wide.size();
   a.bvh_wide = s->wide;
   a.bvh_wtris = s->wtris;
-  a.bvh_wide_lds = (kCoop && nw * sizeof(WideNode) <= (size_t)kBvhLdsNodeBytes) ? (int)nw : 0;
+  a.bvh_wide_lds = (kCoop && nw * kWideF4 * sizeof(float4) <= (size_t)kBvhLdsNodeBytes) ? (int)nw : 0;
   a.coop_stride = 7 * s->host.bvh_wdepth + 8;
   a.bvh_stack = std::max(1, s->host.bvh_depth);
   a.bvh_nbig = (int)s->host.bvh_big_pairs.size();
   a.bvh_big = s->big_pairs;
   a.bvh_big_idx = s->big_idx;
   const size_t head = bvh_lds_offset(base) + (size_t)a.bvh_lds_nodes * sizeof(BvhNode) +
-                      (size_t)a.bvh_wide_lds * sizeof(WideNode) + (size_t)a.bvh_nbig * 6 * sizeof(float);
+                      (size_t)a.bvh_wide_lds * kWideF4 * sizeof(float4) + (size_t)a.bvh_nbig * 6 * sizeof(float);
   if (kCoop) return head + (size_t)(kBlock / 64) * 8 * a.coop_stride * sizeof(uint32_t);
   if (server)
     return head + (size_t)kQFields * kQSlots * sizeof(float) + 8 * sizeof(int) + (size_t)a.bvh_stack * 64 * sizeof(uint32_t);
@@ -1857,7 +1872,7 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
   bv.big_e3 = nullptr;
   bv.nbig = 0;
   CoopView cv;
-  cv.wn = reinterpret_cast<const float4 *>(a.bvh_wide);
+  cv.wn = a.bvh_wide;
   cv.wn_lds = false;
   cv.wt = a.bvh_wtris;
   cv.stk = nullptr;
@@ -1873,12 +1888,11 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
     }
     float4 *lw = ln + 4 * a.bvh_lds_nodes;
     if (kCoop && a.bvh_wide_lds > 0) {
-      const float4 *g = reinterpret_cast<const float4 *>(a.bvh_wide);
-      for (int i = tid; i < 16 * a.bvh_wide_lds; i += kBlock) lw[i] = g[i];
+      for (int i = tid; i < kWideF4 * a.bvh_wide_lds; i += kBlock) lw[i] = a.bvh_wide[i];
       cv.wn = lw;
       cv.wn_lds = true;
     }
-    float *be3 = reinterpret_cast<float *>(lw + 16 * a.bvh_wide_lds);
+    float *be3 = reinterpret_cast<float *>(lw + kWideF4 * a.bvh_wide_lds);
     for (int i = tid; i < 6 * a.bvh_nbig; i += kBlock) {
       const int j = i / 6, kf = (i % 6) >> 1, h = i & 1;
       be3[i] = a.bvh_big[j].f[9 + 4 * kf][h];
