@@ -804,11 +804,14 @@ __device__ __forceinline__ int closest_hit_bvh(const BvhView &B, V3 p, V3 d, flo
 // All lanes of a group hold identical copies of the ray state, so every
 // branch is group-uniform and the DPP reductions (xor 1, xor 2 within quads,
 // half-row mirror) only read lanes of the same, active group.
-// IPT_BVH_QNODES=1 (default): the traversal reads QWideNode (144 B, 9
-// float4) instead of WideNode (256 B, 16 float4): the northstar tree (143
-// nodes) fits the LDS stage; decoding costs ~18 VALU per lane and visit.
+// IPT_BVH_QNODES=1: the traversal reads QWideNode (144 B, 9 float4) instead
+// of WideNode (256 B, 16 float4), so the northstar tree (143 nodes) fits the
+// LDS stage; decoding costs ~18 VALU per lane and visit.  Measured SLOWER
+// (profiles/r02_variants_qnodes.log, C2 size: sphere 6.96 -> 7.41 ms,
+// northstar 8.80 -> 9.04 ms even though its nodes move from L2 to LDS): the
+// cooperative traversal is issue-bound, not fetch-latency-bound.  Off.
 #ifndef IPT_BVH_QNODES
-#define IPT_BVH_QNODES 1
+#define IPT_BVH_QNODES 0
 #endif
 constexpr int kWideF4 = IPT_BVH_QNODES ? 9 : 16;  // float4 per wide node
 struct CoopView {
