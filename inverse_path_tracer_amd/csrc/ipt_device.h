@@ -461,6 +461,34 @@ __device__ __forceinline__ void hit_test_pair(const TriPair &T, int i, V3 p, V3 
 // each costs two v_mov; from LDS (immediate offsets) it costs no VALU.  The
 // unrolled triangle index is an inline constant (no v_mov either).
 constexpr int kSmallPairs = 16;
+// IPT_FAST_CAST=1 (tolerance-mode A/B build, NOT bit-exact): the small-scene
+// loop computes t = num * rcp(-denom) (the 1-ulp reciprocal without the
+// Newton / residual steps of the IEEE division), num = p.n + cn with cn =
+// -(c.n) precomputed per triangle (LDS, after the plane offsets), and drops
+// the |n.d| >= 1e-4 test (a near-parallel plane gives |t| huge or NaN, which
+// the other tests reject but for rare grazing hits): 33 instead of 45 VALU
+// per pair.  Off: the parity build is the product.
+#ifndef IPT_FAST_CAST
+#define IPT_FAST_CAST 0
+#endif
+constexpr int kE3Floats = IPT_FAST_CAST ? 8 : 6;  // LDS floats per pair: 3 plane offsets x 2 (+ cn x 2)
+__device__ __forceinline__ void pair_ray_fast(const TriPair &T, f2 cn, int ia, int ib, V3 p, V3 d, float &bt, int &bi,
+                                              f2 e03, f2 e13, f2 e23) {
+  const f2 n0 = ld2(T, 3), n1 = ld2(T, 4), n2 = ld2(T, 5);
+  const f2 num = fma2(bc2(p.z), n2, fma2(bc2(p.y), n1, fma2(bc2(p.x), n0, cn)));
+  const f2 denom = fma2(n2, bc2(d.z), fma2(n1, bc2(d.y), n0 * bc2(d.x)));
+  const f2 t = num * f2{__builtin_amdgcn_rcpf(-denom.x), __builtin_amdgcn_rcpf(-denom.y)};
+  const f2 qx = fma2(bc2(d.x), t, bc2(p.x)), qy = fma2(bc2(d.y), t, bc2(p.y)), qz = fma2(bc2(d.z), t, bc2(p.z));
+  const f2 s0 = fma2(qz, ld2(T, 8), fma2(qy, ld2(T, 7), fma2(qx, ld2(T, 6), e03)));
+  const f2 s1 = fma2(qz, ld2(T, 12), fma2(qy, ld2(T, 11), fma2(qx, ld2(T, 10), e13)));
+  const f2 s2 = fma2(qz, ld2(T, 16), fma2(qy, ld2(T, 15), fma2(qx, ld2(T, 14), e23)));
+  const bool ta = (t.x >= kEpsUp) & (t.x < bt) & !(fmaxf(fmaxf(s0.x, s1.x), s2.x) > 0.f);
+  bt = ta ? t.x : bt;
+  bi = ta ? ia : bi;
+  const bool tb = (t.y >= kEpsUp) & (t.y < bt) & !(fmaxf(fmaxf(s0.y, s1.y), s2.y) > 0.f);
+  bt = tb ? t.y : bt;
+  bi = tb ? ib : bi;
+}
 __device__ __forceinline__ int closest_hit_pairs_small(const TriPair *__restrict__ pairs, const f2 *e3, int nT,
                                                        V3 p, V3 d, float &best_t) {
   float bt = __builtin_inff();
@@ -482,7 +510,11 @@ __device__ __forceinline__ int closest_hit_pairs_small(const TriPair *__restrict
   for (int j = 0; j < kSmallPairs; ++j) {
     if (j < nP) {  // wave-uniform
       const TriPair T = pairs[j];
+#if IPT_FAST_CAST
+      pair_ray_fast(T, e3l[4 * j + 3], 2 * j, 2 * j + 1, p, d, bt, bi, e3l[4 * j], e3l[4 * j + 1], e3l[4 * j + 2]);
+#else
       pair_ray(T, pair_origin(T, p), 2 * j, 2 * j + 1, p, d, bt, bi, e3l[3 * j], e3l[3 * j + 1], e3l[3 * j + 2]);
+#endif
     }
   }
   best_t = bt;

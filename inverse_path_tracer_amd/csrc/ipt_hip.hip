@@ -414,6 +414,16 @@ __device__ __forceinline__ void srv_serve(const BvhView &B, float *q, const int 
   }
 }
 
+// Entry i of the small-scene LDS table (kE3Floats per pair): the three
+// edge-plane offsets of the pair as (A, B) float pairs, and in the fast-cast
+// build cn = -(c.n) of both triangles.
+__device__ __forceinline__ float small_table_entry(const TriPair *__restrict__ pairs, int i) {
+  const int j = i / kE3Floats, k = i % kE3Floats, h = k & 1;
+  if (k < 6) return pairs[j].f[9 + 4 * (k >> 1)][h];
+  const TriPair &T = pairs[j];
+  return -fmaf(T.f[2][h], T.f[5][h], fmaf(T.f[1][h], T.f[4][h], T.f[0][h] * T.f[3][h]));
+}
+
 // LDS carve-out of the BVH instances: node copy (16-B aligned) + stack.
 __host__ __device__ inline size_t bvh_lds_offset(size_t base) { return (base + 15) & ~(size_t)15; }
 
@@ -485,13 +495,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   float *lds_e3 = tab + (a.kd_tables ? 6 * nT : 0);
   const int nP = (nT + 1) >> 1;
   if (a.small_pairs) {
-    for (int i = tid; i < 6 * nP; i += nthr) {
-      const int j = i / 6, kf = (i % 6) >> 1, h = i & 1;
-      lds_e3[i] = pairs[j].f[9 + 4 * kf][h];
-    }
+    for (int i = tid; i < kE3Floats * nP; i += nthr) lds_e3[i] = small_table_entry(pairs, i);
     e3 = reinterpret_cast<const f2 *>(lds_e3);
   }
-  float *lds_rec = lds_e3 + (a.small_pairs ? 6 * nP : 0);
+  float *lds_rec = lds_e3 + (a.small_pairs ? kE3Floats * nP : 0);
   // Camera-ray ring (RING instances): per wave kRingFields x 64 words after the
   // ADJ records, then the camera origin (3 floats per wave).
   const bool RING = ring_on<MODE, BVH>() && a.use_ring;
@@ -1547,7 +1554,7 @@ static size_t bvh_lds(const GpuScene *s, TraceArgs &a, size_t base, bool server)
 
 static size_t table_bytes(const TraceArgs &a) {
   return (a.kd_tables ? (size_t)6 * a.nT * sizeof(float) : 0) +
-         (a.small_pairs ? (size_t)6 * ((a.nT + 1) / 2) * sizeof(float) : 0);
+         (a.small_pairs ? (size_t)kE3Floats * ((a.nT + 1) / 2) * sizeof(float) : 0);
 }
 
 template <int MODE, bool SPEC, bool BVH>
@@ -1855,10 +1862,7 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
   float *lds_e3 = reinterpret_cast<float *>(lds);
   const f2 *e3 = nullptr;
   if (small) {
-    for (int i = tid; i < 6 * nP; i += kBlock) {
-      const int j = i / 6, kf = (i % 6) >> 1, h = i & 1;
-      lds_e3[i] = pairs[j].f[9 + 4 * kf][h];
-    }
+    for (int i = tid; i < kE3Floats * nP; i += kBlock) lds_e3[i] = small_table_entry(pairs, i);
     e3 = reinterpret_cast<const f2 *>(lds_e3);
   }
   BvhView bv;
@@ -1880,7 +1884,7 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
   for (int k = 0; k < 6; ++k) cv.root[k] = a.root_box[k];
   if (BVH) {
     char *base = reinterpret_cast<char *>(lds);
-    float4 *ln = reinterpret_cast<float4 *>(base + bvh_lds_offset((size_t)(small ? 6 * nP : 0) * sizeof(float)));
+    float4 *ln = reinterpret_cast<float4 *>(base + bvh_lds_offset((size_t)(small ? kE3Floats * nP : 0) * sizeof(float)));
     if (a.bvh_lds_nodes > 0) {
       const float4 *g = reinterpret_cast<const float4 *>(bnodes);
       for (int i = tid; i < 4 * a.bvh_lds_nodes; i += kBlock) ln[i] = g[i];
@@ -1961,7 +1965,7 @@ int gpu_closest_hit(GpuScene *s, int64_t n, const float *org_dev, const float *d
   if (n <= 0) return 0;
   TraceArgs a = make_args_scene(s);
   const int small = (IPT_PAIRS && IPT_SMALL_UNROLL && s->host.nT <= 2 * kSmallPairs) ? 1 : 0;
-  const size_t base = small ? (size_t)6 * ((s->host.nT + 1) / 2) * sizeof(float) : 0;
+  const size_t base = small ? (size_t)kE3Floats * ((s->host.nT + 1) / 2) * sizeof(float) : 0;
   const int blocks = (int)((n + kBlock - 1) / kBlock);
   if (use_bvh(s)) {
     const size_t lds = bvh_lds(s, a, base, false);
