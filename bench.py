@@ -50,7 +50,10 @@ CUBE = ObjectSpec(os.path.join(ASSETS, "shapes", "cube.obj"),
                   "*Kd 0.9041462985304743 0.5854651848798454 0.007022117649276849*", (0, -1.5, 4), (0, 0, 0),
                   (1, 1, 1))
 SCENE0 = CORNELL + [CUBE]
-# the north_star's "+ sphere.obj" scene (not a shipped scene file): 1298 triangles, BVH
+# BASELINE configs[2] as the north_star names it: scenes/0.txt + sphere.obj (assets/northstar.txt), 1310 triangles
+NORTHSTAR = SCENE0 + [ObjectSpec(os.path.join(ASSETS, "shapes", "sphere.obj"), "*Kd 0.2 0.6 0.3*", (-1.2, -1.35, 4.6),
+                                 (0.0, 0.0, 0.0), (1.2, 1.2, 1.2))]
+# the round-1 "+ sphere.obj" scene (Cornell + sphere, no cube): 1298 triangles, BVH
 SPHERE = CORNELL + [ObjectSpec(os.path.join(ASSETS, "shapes", "sphere.obj"), "*Kd 0.2 0.6 0.3*", (0.3, -1.2, 4.2),
                                (0.0, 0.4, 0.0), (1.2, 1.2, 1.2))]
 # casts/sample counted by the CPU oracle over the full C2
@@ -280,6 +283,10 @@ def main():
         # other configurations, this rank's band of an N-way tile split
         for key, objs, w, h, spp, mb, desc in (
                 ("c3", SCENE0, W, H, SPP, BOUNCES, "C3: scenes/0.txt (Cornell + cube, 30 triangles), 512x512, 64 spp, 4 bounces"),
+                ("c3_unbounded", SCENE0, W, H, SPP, None, "C3 with the reference's own estimator (no bounce cap: "
+                 "Russian roulette only), scenes/0.txt, 512x512, 64 spp; adjoint = LDS ring + chunk replay"),
+                ("c3_northstar", NORTHSTAR, W, H, SPP, BOUNCES, "C3 as the north_star names it: Cornell + cube + "
+                 "sphere.obj (assets/northstar.txt, 1310 triangles, BVH), 512x512, 64 spp, 4 bounces"),
                 ("bvh_sphere", SPHERE, W, H, SPP, BOUNCES, "Cornell + sphere.obj (1298 triangles, BVH), 512x512, 64 spp, 4 bounces"),
                 ("c4", SCENE0, 1024, 1024, 256, 8, "C4: scenes/0.txt, 1024x1024, 256 spp, 8 bounces")):
             bb, ee, ss = shard_rows_interleaved(h, world if key != "c4" else 8, rank) if (key != "c4" or world <= 8) \

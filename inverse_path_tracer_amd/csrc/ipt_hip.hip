@@ -54,7 +54,17 @@ const char *gpu_last_error() { return g_gpu_err.c_str(); }
     }                                                                                        \
   } while (0)
 
-enum { MODE_FWD = 0, MODE_ADJ = 1, MODE_GRAPH = 2 };
+// MODE_ADJU: the adjoint of the reference's own estimator (no bounce cap,
+// paths end by Russian roulette or a miss, path_trace.cu:172-181).  Vertex
+// records live in an LDS ring of rec_cap slots; a path longer than the ring
+// is swept in chunks from its end, each earlier chunk re-recorded by
+// replaying the path from its camera ray (same seed, same draws, so the same
+// floats) -- see trace_kernel.
+enum { MODE_FWD = 0, MODE_ADJ = 1, MODE_GRAPH = 2, MODE_ADJU = 3 };
+template <int MODE>
+constexpr bool is_adj() {
+  return MODE == MODE_ADJ || MODE == MODE_ADJU;
+}
 constexpr int kBlock = 256;
 // Adjoint vertex record (per lane, in LDS): tri | et << 16, the emitter factor
 // s (lo = Ke[et] * s is rebuilt bit-identically in the sweep; s = 0 when the
@@ -83,6 +93,15 @@ __host__ __device__ inline size_t graph_lds_doubles(int nT, int nE) {
   return (size_t)(nT + 1) * nT * kEdgeL + (size_t)(nT + 1) * (nE > 0 ? nE : 0) * 3;
 }
 constexpr int kMaxAdjBounces = 62;
+// ADJU ring slots per lane: 8 x 3 words x 256 lanes = 24 KB of LDS (6
+// workgroups per CU).  Paths of more than 8 vertices replay their earlier
+// chunks (Russian roulette keeps 90% per bounce and the box is open at the
+// front, so long paths are a small minority; a path of K vertices costs
+// about K^2 / 16 extra vertex traces).
+#ifndef IPT_ADJU_RING
+#define IPT_ADJU_RING 8
+#endif
+constexpr int kAdjuRing = IPT_ADJU_RING;
 constexpr int kMaxTableTris = 512;  // kd/kd-over-pi LDS tables up to 12 KB
 #ifndef IPT_LDS_GRAD_KB
 #define IPT_LDS_GRAD_KB 12
@@ -144,6 +163,7 @@ struct TraceArgs {
   // float x: both are the correctly rounded x * 2^-k), else 0
   float rc_spp;
   int use_ring;  // RING instances: camera rays from the LDS ring (host decides: only if it costs no residency)
+  int rec_cap;   // ADJ: vertex records per lane (max_bounces + 1); ADJU: ring slots
   // scene batch (C5): blocks [b * bps, (b+1) * bps) trace material set b --
   // kd + b*3nT, seed + b*seed_stride, outputs at b * (out|adj)_stride,
   // gradient at b*3nT -- so each workgroup holds ONE set's tables and bins
@@ -261,8 +281,8 @@ __device__ __forceinline__ void item_ray(const TraceArgs &a, uint64_t seed, uint
 #endif
 template <int MODE, bool BVH>
 constexpr int min_blocks() {
-  return BVH ? (MODE == 1 ? IPT_MIN_BLOCKS_BVH_ADJ : (MODE == 0 ? IPT_MIN_BLOCKS_BVH_FWD : IPT_MIN_BLOCKS_BVH))
-             : (MODE == 0 ? IPT_MIN_BLOCKS_FWD : (MODE == 1 ? IPT_MIN_BLOCKS_ADJ : IPT_MIN_BLOCKS_GRAPH));
+  return BVH ? (is_adj<MODE>() ? IPT_MIN_BLOCKS_BVH_ADJ : (MODE == 0 ? IPT_MIN_BLOCKS_BVH_FWD : IPT_MIN_BLOCKS_BVH))
+             : (MODE == 0 ? IPT_MIN_BLOCKS_FWD : (is_adj<MODE>() ? IPT_MIN_BLOCKS_ADJ : IPT_MIN_BLOCKS_GRAPH));
 }
 // IPT_BVH_SERVER=1: BVH instances run 4 path waves + 1 traversal-server
 // wave per workgroup (ray compaction through an LDS queue, see trace_kernel).
@@ -445,7 +465,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   if (a.nscenes > 1) {
     kd += (size_t)set * 3 * a.nT;
     if (MODE == MODE_FWD) out_samples += (size_t)set * a.out_stride;
-    if (MODE == MODE_ADJ) {
+    if (is_adj<MODE>()) {
       adj += (size_t)set * a.adj_stride;
       grad += (size_t)set * 3 * a.nT;
     }
@@ -454,11 +474,11 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   constexpr bool SERVE = BVH && IPT_BVH_SERVER;  // + a traversal-server wave
   constexpr int nthr = block_threads<BVH>();
   const int nT = a.nT, nE = a.nE;
-  const int vmax = a.max_bounces + 1;  // ADJ record capacity per lane
+  const int vmax = a.rec_cap;  // ADJ record capacity per lane (ADJU: ring slots)
   // LDS: [fp64 accumulators][kd table][kd/pi table][ADJ vertex records]
   double *lds_acc = lds;               // ADJ: nT*3 grad; GRAPH: (nT+1)*nT*kEdgeW bins
   int n_acc = 0;
-  if (MODE == MODE_ADJ) {
+  if (is_adj<MODE>()) {
     n_acc = a.grad_slots * 3;
   } else if (MODE == MODE_GRAPH && a.lds_edges) {
     n_acc = (int)graph_lds_doubles(nT, nE);
@@ -504,7 +524,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   const bool RING = ring_on<MODE, BVH>() && a.use_ring;
   float *ring = nullptr;
   if (RING) {
-    const size_t rec_words = (MODE == MODE_ADJ) ? (size_t)vmax * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock : 0;
+    const size_t rec_words = is_adj<MODE>() ? (size_t)vmax * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock : 0;
     ring = lds_rec + rec_words + (size_t)(tid >> 6) * (kRingFields * 64 + 4);
   }
   BvhView bv;
@@ -527,7 +547,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   float *srvq = nullptr;  // SERVE: ray queue [kQFields][kQSlots]
   int *srvc = nullptr;    // SERVE: per path wave queued count [4], live flag [4]
   if (BVH) {
-    const size_t rec_words = (MODE == MODE_ADJ) ? (size_t)vmax * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock : 0;
+    const size_t rec_words = is_adj<MODE>() ? (size_t)vmax * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock : 0;
     char *base = reinterpret_cast<char *>(lds);
     const size_t off = bvh_lds_offset((size_t)(reinterpret_cast<char *>(lds_rec + rec_words) - base));
     float4 *ln = reinterpret_cast<float4 *>(base + off);
@@ -596,6 +616,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   Rng st;
   V3 p = mk(0.f, 0.f, 0.f), d = p;
   V3 L = p, Le = p, Ld = p, M = mk(1.f, 1.f, 1.f);
+  // ADJU (unbounded adjoint): throughput at the oldest ring record, suffix
+  // carried from the chunk after, replay target (0 = first pass), next slot
+  V3 Mlo = M, Scar = mk(0.f, 0.f, 0.f);
+  int rhi = 0, rslot = 0;
   float weight = 1.f;  // GRAPH path weight
   V3 pix = p;          // GRAPH target pixel
   int k = 0, dst = 0;
@@ -690,6 +714,11 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           Ld = L;
           M = mk(1.f, 1.f, 1.f);
           k = 0;
+          if (MODE == MODE_ADJU) {
+            Mlo = M;
+            rhi = 0;
+            rslot = 0;
+          }
           if (MODE == MODE_GRAPH) {
             weight = 1.f;
             dst = nT;
@@ -929,6 +958,29 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           rec[(kRecSD + 1) * fs] = speci;
         }
       }
+      if (MODE == MODE_ADJU) {  // ring slot rslot = k % rec_cap; evicting vertex k - rec_cap folds it into Mlo
+        float *rec = lds_rec + (size_t)rslot * kBlock + tid;
+        const size_t fs = (size_t)vmax * kBlock;
+        if (k >= vmax) {  // Mlo <- M_{k - rec_cap + 1}, with the forward's own operations
+          const int tj = (int)(__float_as_uint(rec[0]) & 0xffffu);
+          const float cj = rec[2 * fs];
+          V3 tv = kdpi3(tj);
+          if (SPEC) {
+            const TriMat &mj = mat[tj];
+            const float si = rec[(kRecSD + 1) * fs];
+            tv = mk(tv.x + mj.ks[0] * si, tv.y + mj.ks[1] * si, tv.z + mj.ks[2] * si);
+          }
+          Mlo = mk((Mlo.x * tv.x) * cj, (Mlo.y * tv.y) * cj, (Mlo.z * tv.z) * cj);
+        }
+        rec[0] = __uint_as_float((uint32_t)tri | ((uint32_t)emit_et << 16));
+        rec[fs] = emit_s;
+        rec[2 * fs] = coeff;
+        if (SPEC) {
+          rec[kRecSD * fs] = specd;
+          rec[(kRecSD + 1) * fs] = speci;
+        }
+        rslot = (rslot + 1 == vmax) ? 0 : rslot + 1;
+      }
       if (MODE == MODE_GRAPH) {
         if (cont) {
           weight *= dot3(nd, nh);  // inv_path_trace.cu:144-145
@@ -952,6 +1004,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       ++k;  // vertices so far
       if (cont) d = nd;
       else finished = true;
+      if (MODE == MODE_ADJU && rhi > 0 && k == rhi) finished = true;  // replay reached its chunk's end
     }
 
     if (finished) {
@@ -961,6 +1014,102 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         o[0] = L.x;
         o[1] = L.y;
         o[2] = L.z;
+      } else if (MODE == MODE_ADJU) {
+        // Sweep the chunk [lo, hi) held by the ring: hi = K (first pass; the
+        // escape terms of the path's end apply) or the replay target.  Same
+        // operations as the per-lane sweep below / the oracle's
+        // adjoint_sample: prefix throughputs folded from Mlo = M_lo, the
+        // suffix S from the chunk after (Scar) or the escape term.
+        const bool first = rhi == 0;
+        const int hi = first ? k : rhi;
+        const int lo = hi > vmax ? hi - vmax : 0;
+        if (hi > 0) {
+          const size_t fs = (size_t)vmax * kBlock;
+          const uint64_t pixel = item_pixel(a, witem);
+          const float ax = adj[pixel * 3 + 0] / (float)a.spp;
+          const float ay = adj[pixel * 3 + 1] / (float)a.spp;
+          const float az = adj[pixel * 3 + 2] / (float)a.spp;
+          auto col = [&](int v) {  // record of vertex v in [lo, hi): ring slot v % rec_cap
+            int sl = rslot - (hi - v);
+            sl = sl < 0 ? sl + vmax : sl;
+            return lds_rec + (size_t)sl * kBlock + tid;
+          };
+          auto rec_lo = [&](const float *r) {  // the forward's lo, same products
+            const TriMat &me = mat[__float_as_uint(r[0]) >> 16];
+            return mk(me.ke[0] * r[fs], me.ke[1] * r[fs], me.ke[2] * r[fs]);
+          };
+          auto tdiff = [&](const float *r) {  // T_j = kd/pi (+ Ks*speci)
+            const int tj = (int)(__float_as_uint(r[0]) & 0xffffu);
+            V3 x = kdpi3(tj);
+            if (SPEC) {
+              const TriMat &mj = mat[tj];
+              const float si = r[(kRecSD + 1) * fs];
+              x = mk(x.x + mj.ks[0] * si, x.y + mj.ks[1] * si, x.z + mj.ks[2] * si);
+            }
+            return x;
+          };
+          auto ddir = [&](const float *r) {  // D_j = kd (+ Ks*specd)
+            const int tj = (int)(__float_as_uint(r[0]) & 0xffffu);
+            V3 x = kd3(tj);
+            if (SPEC) {
+              const TriMat &mj = mat[tj];
+              const float sd = r[kRecSD * fs];
+              x = mk(x.x + mj.ks[0] * sd, x.y + mj.ks[1] * sd, x.z + mj.ks[2] * sd);
+            }
+            return x;
+          };
+          V3 S = Scar;
+          if (first) {
+            S = mk(0.f, 0.f, 0.f);
+            if (escaped) {
+              const float *r = col(hi - 1);
+              const V3 lk = rec_lo(r), dj = ddir(r);
+              S = mk(Le.x + dj.x * lk.x, Le.y + dj.y * lk.y, Le.z + dj.z * lk.z);
+            }
+          }
+          for (int kk = hi - 1; kk >= lo; --kk) {
+            V3 Mk = Mlo;
+            for (int j = lo; j < kk; ++j) {
+              const float *rj = col(j);
+              const float cj = rj[2 * fs];
+              const V3 tv = tdiff(rj);
+              Mk = mk((Mk.x * tv.x) * cj, (Mk.y * tv.y) * cj, (Mk.z * tv.z) * cj);
+            }
+            const float *r = col(kk);
+            const int tk = (int)(__float_as_uint(r[0]) & 0xffffu);
+            const V3 lk = rec_lo(r);
+            const float ck = r[2 * fs];
+            const bool last_esc = first && escaped && kk == hi - 1;
+            const bool continued = !first || kk < hi - 1 || escaped;
+            V3 dLd = Mk;
+            if (last_esc) dLd = mk(dLd.x + M.x, dLd.y + M.y, dLd.z + M.z);
+            V3 gk = mk(dLd.x * lk.x, dLd.y * lk.y, dLd.z * lk.z);
+            if (continued) {
+              const float cpi = ck / kPiF;
+              gk = mk(gk.x + (cpi * Mk.x) * S.x, gk.y + (cpi * Mk.y) * S.y, gk.z + (cpi * Mk.z) * S.z);
+            }
+            const int sl = a.grad_map ? a.grad_map[tk] : tk;
+            const double v[3] = {(double)(ax * gk.x), (double)(ay * gk.y), (double)(az * gk.z)};
+            bins_add(sl >= 0, grad, sl >= 0 ? (size_t)sl * 3 : (size_t)tk * 3, 3, v);
+            const V3 dj = ddir(r), tv = tdiff(r);
+            S = mk((Le.x + dj.x * lk.x) + (tv.x * ck) * S.x, (Le.y + dj.y * lk.y) + (tv.y * ck) * S.y,
+                   (Le.z + dj.z * lk.z) + (tv.z * ck) * S.z);
+          }
+          Scar = S;  // S_lo: the suffix the previous chunk's last vertex continues into
+        }
+        if (lo > 0) {  // replay the path from its camera ray to re-record [lo - rec_cap, lo)
+          int r, c;
+          item_ray(a, seed, witem, st, p, d, r, c);
+          L = mk(0.f, 0.f, 0.f);
+          Le = L;
+          Ld = L;
+          M = mk(1.f, 1.f, 1.f);
+          Mlo = M;
+          k = 0;
+          rslot = 0;
+          rhi = lo;
+          active = true;
+        }
       } else if (MODE == MODE_ADJ && !IPT_ADJ_WAVE_SWEEP) {
         // backward sweep over the recorded vertices (oracle adjoint_sample)
         const int K = k;
@@ -1186,11 +1335,11 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   if (MODE != MODE_FWD) {
     __syncthreads();
     if (n_acc > 0) {
-      double *dstp = (MODE == MODE_ADJ) ? grad : edges;
+      double *dstp = is_adj<MODE>() ? grad : edges;
       const int nb5 = (nT + 1) * nT * kEdgeL;
       for (int i = tid; i < n_acc; i += nthr) {
         const double v = lds_acc[i];
-        int j = (MODE == MODE_ADJ && a.slot_tri) ? a.slot_tri[i / 3] * 3 + i % 3 : i;
+        int j = (is_adj<MODE>() && a.slot_tri) ? a.slot_tri[i / 3] * 3 + i % 3 : i;
         if (MODE == MODE_GRAPH) {  // LDS form -> kEdgeW-wide global bins
           if (i < nb5) {
             j = (i / kEdgeL) * kEdgeW + i % kEdgeL;
@@ -1280,8 +1429,8 @@ struct GpuScene {
   TriIsect *wtris = nullptr;
   int accel = IPT_ACCEL_AUTO;
   int *grad_map = nullptr, *slot_tri = nullptr;  // ADJ hot-set LDS slots (large scenes)
-  int grid[12] = {0};       // resident workgroups per (mode, spec, bvh) (0 = not queried)
-  size_t grid_lds[12] = {0};
+  int grid[16] = {0};       // resident workgroups per (mode, spec, bvh) (0 = not queried)
+  size_t grid_lds[16] = {0};
 };
 
 #ifdef IPT_PHASE_TIMING
@@ -1511,6 +1660,7 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.slot_tri = nullptr;
   std::memcpy(a.cam, s->host.cam, sizeof a.cam);
   a.use_ring = 0;
+  a.rec_cap = p.max_bounces >= 0 ? p.max_bounces + 1 : 0;
   a.nscenes = p.nscenes > 1 ? p.nscenes : 1;
   a.bps = 1;
   a.seed_stride = p.seed_stride;
@@ -1693,10 +1843,11 @@ int gpu_render(GpuScene *s, const RenderParams &p, const float *kd_dev, float *h
 int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const float *adj_dev, double *grad_dev,
                 void *stream) {
   if (check_params(s, p)) return -1;
-  if (p.max_bounces < 0 || p.max_bounces > kMaxAdjBounces) {
-    gpu_set_error("adjoint requires 0 <= max_bounces <= 62 (vertex records live in LDS)");
+  if (p.max_bounces > kMaxAdjBounces) {
+    gpu_set_error("adjoint requires max_bounces <= 62 (vertex records live in LDS); -1 = unbounded");
     return -1;
   }
+  const bool unbounded = p.max_bounces < 0;
   if (s->host.nT > kMaxAdjTris) {
     gpu_set_error("adjoint supports at most 65535 triangles");
     return -1;
@@ -1710,13 +1861,15 @@ int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const f
   } else {
     a.grad_slots = s->host.nT;
   }
+  if (unbounded) a.rec_cap = kAdjuRing;
   const size_t lds = (size_t)a.grad_slots * 3 * sizeof(double) + table_bytes(a) +
-                     (size_t)(p.max_bounces + 1) * (s->has_ks ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock *
-                         sizeof(float);
+                     (size_t)a.rec_cap * (s->has_ks ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock * sizeof(float);
   if (lds > 160 * 1024) {
     gpu_set_error("adjoint LDS footprint exceeds 160 KiB; lower max_bounces");
     return -1;
   }
+  if (unbounded)
+    return launch<MODE_ADJU>(s, a, lds, kd_dev, nullptr, adj_dev, grad_dev, nullptr, nullptr, (hipStream_t)stream);
   return launch<MODE_ADJ>(s, a, lds, kd_dev, nullptr, adj_dev, grad_dev, nullptr, nullptr, (hipStream_t)stream);
 }
 

@@ -79,7 +79,9 @@ def _replay_params(p: N.Params, adjoint_seed):
 def render(scene: Scene, kd: torch.Tensor, width: int, height: int, spp: int, max_bounces=4, seed: int = 0,
            row_begin: int = 0, row_end=None, adjoint_seed=None, row_step: int = 1) -> torch.Tensor:
     """Differentiable render: HDR image of rows row_begin, row_begin + row_step,
-    ... < row_end w.r.t. kd.
+    ... < row_end w.r.t. kd.  max_bounces None is the reference's own
+    estimator (paths end by Russian roulette or a miss); its adjoint keeps
+    the vertex records in an LDS ring and replays long paths chunk by chunk.
 
     The backward pass replays the forward's paths (adjoint_seed None) or
     traces the same configuration with seed `adjoint_seed`.  The second form
@@ -94,8 +96,6 @@ def render(scene: Scene, kd: torch.Tensor, width: int, height: int, spp: int, ma
     of the five state words and their first draws differ only by a constant
     -- correlated streams (measured: a residual bias of ~14% of the
     same-stream one, tests/test_gpu_full.py)."""
-    if max_bounces is None and kd.requires_grad:
-        raise ValueError("the adjoint needs a finite max_bounces (vertex records live in LDS)")
     p = N.make_params(width, height, spp, max_bounces, seed, row_begin, row_end, row_step)
     return _RenderFn.apply(kd, scene, p, adjoint_seed)
 
@@ -131,8 +131,6 @@ def render_batch(scene: Scene, kd: torch.Tensor, width: int, height: int, spp: i
     Set b is ``render(scene, kd[b], ..., seed + b * seed_stride)`` bit for bit
     (default stride: one frame of samples, so the sets' sample streams are
     disjoint); the backward runs ONE batched adjoint launch."""
-    if max_bounces is None and kd.requires_grad:
-        raise ValueError("the adjoint needs a finite max_bounces (vertex records live in LDS)")
     if kd.dim() != 3 or kd.shape[1] != scene.nT or kd.shape[2] != 3:
         raise ValueError("kd must be (S, nT=%d, 3), got %s" % (scene.nT, tuple(kd.shape)))
     stride = width * height * spp if seed_stride is None else int(seed_stride)

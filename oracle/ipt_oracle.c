@@ -1412,7 +1412,7 @@ static void trace_forward(const oscene_t *sc, int W, int H, int spp, int max_bou
       } else {
         Ld[0] = Ld[1] = Ld[2] = 0.f;
       }
-      vrec_t *vr = (rec && n <= max_bounces) ? &rec[n] : NULL;
+      vrec_t *vr = (rec && (max_bounces < 0 || n <= max_bounces)) ? &rec[n] : NULL;
       if (vr) {
         vr->tri = h.tri;
         for (int i = 0; i < 3; i++)
@@ -1608,18 +1608,40 @@ int oro_graph(void *p, int W, int H, int spp, int max_bounces, uint64_t seed, in
 /* ------------------------------------------------------------------ */
 /* adjoint (new capability)                             */
 /* ------------------------------------------------------------------ */
+/* Per-thread record storage of the adjoint: max_bounces + 1 records, or for
+ * unbounded paths (max_bounces < 0, the reference's own estimator) as many as
+ * the path has -- counted by a first trace, then the same path traced again
+ * with records (same seed, same draws). */
+typedef struct {
+  vrec_t *rec;
+  float (*Mk)[3];
+  int cap;
+} adj_buf_t;
+static void adj_buf_reserve(adj_buf_t *b, int n) {
+  if (n <= b->cap) return;
+  b->cap = n + 16;
+  b->rec = (vrec_t *)realloc(b->rec, sizeof(vrec_t) * (size_t)b->cap);
+  b->Mk = (float(*)[3])realloc(b->Mk, sizeof(float[3]) * (size_t)(b->cap + 1));
+}
 static void adjoint_sample(const oscene_t *sc, int W, int H, int spp, int max_bounces,
                            uint64_t seed, int64_t gidx, const float *adj, double *grad,
-                           vrec_t *rec) {
+                           adj_buf_t *buf) {
   float L[3];
   int K = 0, esc = 0;
+  if (max_bounces < 0) { /* unbounded: length first */
+    trace_forward(sc, W, H, spp, max_bounces, seed, gidx, L, NULL, NULL, &K, &esc);
+    adj_buf_reserve(buf, K);
+  } else {
+    adj_buf_reserve(buf, max_bounces + 1);
+  }
+  vrec_t *rec = buf->rec;
   trace_forward(sc, W, H, spp, max_bounces, seed, gidx, L, NULL, rec, &K, &esc);
   if (K == 0) return;
   int64_t pix = gidx / spp;
   float a[3];
   for (int i = 0; i < 3; i++) a[i] = adj[pix * 3 + i] / (float)spp;
   const float *Le = sc->tris[rec[0].tri].m.emission;
-  float Mk[64][3]; /* prefix throughputs M_0..M_K */
+  float(*Mk)[3] = buf->Mk; /* prefix throughputs M_0..M_K */
   for (int i = 0; i < 3; i++) Mk[0][i] = 1.f;
   for (int k = 0; k < K; k++) {
     const omat_t *m = &sc->tris[rec[k].tri].m;
@@ -1658,9 +1680,8 @@ static void adjoint_sample(const oscene_t *sc, int W, int H, int spp, int max_bo
 int oro_adjoint(void *p, int W, int H, int spp, int max_bounces, uint64_t seed, int row_begin,
                 int row_end, const float *adj, double *grad) {
   oscene_t *sc = (oscene_t *)p;
-  if (!sc || max_bounces < 0 || max_bounces > 62 || row_begin < 0 || row_end > H ||
-      row_begin > row_end) {
-    set_err("bad adjoint arguments (max_bounces must be in [0, 62])");
+  if (!sc || max_bounces > 62 || row_begin < 0 || row_end > H || row_begin > row_end) {
+    set_err("bad adjoint arguments (max_bounces must be <= 62; < 0 = unbounded)");
     return -1;
   }
   size_t ng = (size_t)sc->nT * 3;
@@ -1676,11 +1697,13 @@ int oro_adjoint(void *p, int W, int H, int spp, int max_bounces, uint64_t seed, 
 #else
     int tid = 0, nt = 1;
 #endif
-    vrec_t rec[64];
+    adj_buf_t buf = {NULL, NULL, 0};
     int64_t chunk = (n + nt - 1) / nt;
     int64_t lo = b + chunk * tid, hi = lo + chunk < e ? lo + chunk : e;
     for (int64_t g = lo; g < hi; g++)
-      adjoint_sample(sc, W, H, spp, max_bounces, seed, g, adj, gs + ng * (size_t)tid, rec);
+      adjoint_sample(sc, W, H, spp, max_bounces, seed, g, adj, gs + ng * (size_t)tid, &buf);
+    free(buf.rec);
+    free(buf.Mk);
   }
   for (size_t i = 0; i < ng; i++) {
     double s = 0.0;

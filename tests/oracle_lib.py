@@ -156,7 +156,8 @@ class OracleScene:
         row_end = H if row_end is None else row_end
         adj = np.ascontiguousarray(adj, np.float32).reshape(H, W, 3)
         grad = np.zeros((self.nT, 3), np.float64)
-        rc = self.L.oro_adjoint(self.ptr, W, H, spp, max_bounces, seed, row_begin, row_end, _fp(adj), _dp(grad))
+        rc = self.L.oro_adjoint(self.ptr, W, H, spp, -1 if max_bounces is None else max_bounces, seed, row_begin,
+                                row_end, _fp(adj), _dp(grad))
         if rc:
             raise RuntimeError(self.L.oro_last_error().decode())
         return grad

@@ -115,7 +115,7 @@ def test_empty_band_and_bad_params(scenes):
     with pytest.raises(NativeError):
         P.render(16, 16, 2, 2, 0, row_begin=3, row_end=20)
     with pytest.raises(NativeError, match="max_bounces"):
-        P.adjoint(np.zeros((8, 8, 3), np.float32), 8, 8, 1, None, 0)
+        P.adjoint(np.zeros((8, 8, 3), np.float32), 8, 8, 1, 63, 0)
 
 
 # ------------------------------------------------------------- sharding (C2/C4 sizes)
@@ -136,7 +136,9 @@ def test_row_band_sharding_bit_exact(scenes, W, H, spp, mb, world):
 @pytest.mark.parametrize("name,W,H,spp,mb,seed", [
     ("scene0", 64, 64, 8, 4, 3), ("scene0", 31, 23, 4, 8, 1), ("cornell", 48, 48, 8, 2, 6), ("scene0", 16, 16, 4, 0, 2),
     # spp not a power of two (the weight division path), long paths (many sweep tasks per lane)
-    ("scene0", 20, 12, 3, 5, 5), ("cornell", 24, 16, 5, 20, 7)])
+    ("scene0", 20, 12, 3, 5, 5), ("cornell", 24, 16, 5, 20, 7),
+    # the reference's own estimator (no cap): ring records + chunk replays of paths longer than the ring
+    ("scene0", 64, 64, 8, None, 3), ("cornell", 33, 21, 16, None, 9)])
 def test_adjoint_matches_oracle(scenes, name, W, H, spp, mb, seed):
     P, Q = scenes[name]
     adj = np.random.RandomState(seed).uniform(-1, 1, (H, W, 3)).astype(np.float32)

@@ -179,6 +179,44 @@ def test_adjoint_matches_central_differences(oracle):
     assert np.all(g[16:18] == g[16:18])  # finite everywhere
 
 
+def test_unbounded_adjoint_matches_central_differences(oracle):
+    """The adjoint of the reference's own estimator (no bounce cap; paths end
+    by Russian roulette or a miss, path_trace.cu:172-181) against central
+    differences of the unbounded forward under common random numbers."""
+    W = H = 16
+    spp, seed = 4, 8
+    sc = oracle.OracleScene(SCENE0)
+    adj = np.random.RandomState(4).uniform(-1, 1, (H, W, 3)).astype(np.float32)
+    g = sc.adjoint(W, H, spp, None, seed, adj)
+    kd0 = sc.get_materials()
+
+    def loss(kd):
+        sc.set_materials(kd)
+        hdr, _, _ = sc.render(W, H, spp, None, seed)
+        return float((adj.astype(np.float64) * hdr.astype(np.float64)).sum())
+
+    h = 1e-2
+    for (t, c) in [(0, 0), (4, 1), (10, 2), (12, 0), (14, 1), (20, 2), (27, 0)]:
+        kp, km = kd0.copy(), kd0.copy()
+        kp[t, c] += h
+        km[t, c] -= h
+        fd = (loss(kp) - loss(km)) / (2 * h)
+        assert abs(fd - g[t, c]) <= 2e-3 * max(1.0, abs(g[t, c])), (t, c, fd, g[t, c])
+    sc.set_materials(kd0)
+
+
+def test_unbounded_adjoint_equals_capped_when_no_path_reaches_the_cap(oracle):
+    """max_bounces = 62 differs from the unbounded estimator only for paths
+    of more than 62 bounces (they stop before the 63rd roulette draw); a small
+    frame has none, so the two adjoints (fixed record array vs per-path
+    buffer) must agree to summation order."""
+    sc = oracle.OracleScene(SCENE0)
+    adj = np.random.RandomState(5).uniform(-1, 1, (12, 12, 3)).astype(np.float32)
+    a = sc.adjoint(12, 12, 8, None, 3, adj)
+    b = sc.adjoint(12, 12, 8, 62, 3, adj)
+    np.testing.assert_allclose(a, b, rtol=1e-12, atol=1e-15)
+
+
 # ----------------------------------------------------------------- graph
 def _compress_np(nT, acc):
     """numpy restatement of DataWrapper::compress (inv_scene.h:87-115)."""
