@@ -64,6 +64,25 @@ N_TRIANGLES = 18
 FLOP_PER_TEST = 38          # F1 test with hoisted edge planes
 PEAK_FP32_TFLOPS = 157.3    # MI355X FP32 vector (= FP32 MFMA) peak, MI355X_MICROARCH.md
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_fwd_trace_kernel.json")
+# algorithmic FLOP per sample of the other lines: brute force
+# = C_bar * nT * 38 (C3's C_bar from tools/count_casts.py); BVH scenes = the
+# tests actually executed, counted by the IPT_BVH_STATS build
+# (tools/bvh_stats.py -> profiles/bvh_stats.json: 38 per triangle test + 12
+# per slab test)
+CASTS_PER_SAMPLE_C3 = 5.61259913444519
+BVH_STATS_FILE = os.path.join(ROOT, "profiles", "bvh_stats.json")
+
+
+def flop_per_sample(key):
+    if key == "c3":
+        return CASTS_PER_SAMPLE_C3 * 30 * FLOP_PER_TEST, "C_bar(C3) * 30 * 38"
+    name = {"c3_northstar": "northstar", "bvh_sphere": "sphere"}.get(key)
+    if name and os.path.exists(BVH_STATS_FILE):
+        with open(BVH_STATS_FILE) as f:
+            st = json.load(f)
+        if name + "_fwd" in st:
+            return st[name + "_fwd"]["derived"]["flop_per_sample"], "executed BVH tests (profiles/bvh_stats.json)"
+    return None, None
 
 
 def parse():
@@ -298,6 +317,13 @@ def main():
             f = cx.timed(lambda i: leg.fwd(i), reps) / reps
             a = cx.timed(lambda i: leg.adjoint(i), reps) / reps
             n = leg.samples_per_call() * world
+            fps, how = flop_per_sample(key)
+            if fps:  # per rank: this rank's samples over its own kernel time
+                extra[key + "_roofline"] = {
+                    "bound": "valu", "unit": "TFLOP/s", "peak": PEAK_FP32_TFLOPS, "flop_per_sample": round(fps, 2),
+                    "flop_source": how,
+                    "fwd_frac": round(leg.samples_per_call() * fps / (f / 1e3) / 1e12 / PEAK_FP32_TFLOPS, 4),
+                    "adj_frac": round(leg.samples_per_call() * fps / (a / 1e3) / 1e12 / PEAK_FP32_TFLOPS, 4)}
             extra[key] = {"value": round(n / f / 1e3, 2), "unit": "Msamples/s", "grad_value": round(n / a / 1e3, 2),
                           "grad_unit": "grad-Msamples/s", "fwd_ms": round(f, 4), "adj_ms": round(a, 4),
                           "triangles": leg.sc.nT, "accel": leg.sc.bvh_info()["accel"],
@@ -317,6 +343,8 @@ def main():
     band_samples = head.samples_per_call()
     flop_per_launch = band_samples * CASTS_PER_SAMPLE * N_TRIANGLES * FLOP_PER_TEST
     achieved = flop_per_launch / (kernel_ms / 1e3) / 1e12
+    # the adjoint kernel over the same casts (its step also holds the gradient memset + all-reduce)
+    grad_achieved = flop_per_launch / (bwd_ms / args.steps / 1e3) / 1e12
     traffic = None
     if os.path.exists(PMC_FILE):
         with open(PMC_FILE) as f:
@@ -333,6 +361,7 @@ def main():
                 "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
                 "kernel": "trace_kernel<MODE_FWD>", "kernel_ms": round(kernel_ms, 4),
                 "flop_per_launch": flop_per_launch,
+                "grad_achieved": round(grad_achieved, 3), "grad_frac": round(grad_achieved / PEAK_FP32_TFLOPS, 4),
                 "formula": "samples*C_bar(%.4f)*nT(%d)*38 FLOP / kernel time; peak = FP32 vector peak (equal to "
                            "the FP32 MFMA peak on gfx950)" % (CASTS_PER_SAMPLE, N_TRIANGLES)}
     cpu = None
