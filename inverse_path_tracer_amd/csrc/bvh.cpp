@@ -382,6 +382,25 @@ static bool build_wide(HostScene *S) {
       }
       std::memcpy(&sl[6], &ref, sizeof ref);
     }
+    // Front-to-back child order per ray-direction octant o (bit a set: d_a <
+    // 0), 3 bits per rank, kept in slot o's pad word: rank by the centre's
+    // coordinate sum signed by the octant, empty slots last.  Only the visit
+    // order of the octant-ordered traversal (IPT_BVH_OCTANT) depends on it.
+    for (int o = 0; o < 8; ++o) {
+      int order[8];
+      double key[8];
+      for (int k = 0; k < 8; ++k) {
+        order[k] = k;
+        key[k] = k < (int)kids.size() ? 0.0 : HUGE_VAL;
+        if (k < (int)kids.size())
+          for (int a = 0; a < 3; ++a)
+            key[k] += ((o >> a) & 1 ? -0.5 : 0.5) * ((double)kids[(size_t)k].lo[a] + kids[(size_t)k].hi[a]);
+      }
+      std::stable_sort(order, order + 8, [&](int x, int y) { return key[x] < key[y]; });
+      uint32_t perm = 0;
+      for (int r = 0; r < 8; ++r) perm |= (uint32_t)order[r] << (3 * r);
+      std::memcpy(&W.s[o][7], &perm, sizeof perm);
+    }
     S->bvh_wide.push_back(W);
   }
   return true;

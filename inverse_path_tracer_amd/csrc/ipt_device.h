@@ -846,6 +846,13 @@ __device__ __forceinline__ int closest_hit_bvh(const BvhView &B, V3 p, V3 d, flo
 #define IPT_BVH_QNODES 0
 #endif
 constexpr int kWideF4 = IPT_BVH_QNODES ? 9 : 16;  // float4 per wide node
+// IPT_BVH_OCTANT=1: lane j of a group tests the child of rank j in the ray
+// octant's precomputed front-to-back order (bvh.cpp, slot o's pad word), so
+// the next node is the lowest set bit of the hit mask -- no DPP distance
+// reduction per visit (~15 VALU), one extra dependent LDS read.
+#ifndef IPT_BVH_OCTANT
+#define IPT_BVH_OCTANT 0
+#endif
 struct CoopView {
   const float4 *wn;    // wide nodes (WideNode or QWideNode, kWideF4 float4 each)
   bool wn_lds;         // wn points into LDS (else global memory)
@@ -938,6 +945,8 @@ __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3
     if (src >= 0) {
       const int target = gi;
       const SlabRay r = slab_ray(gp, gd);
+      const int oct = (gd.x < 0.f ? 1 : 0) | (gd.y < 0.f ? 2 : 0) | (gd.z < 0.f ? 4 : 0);  // IPT_BVH_OCTANT
+      (void)oct;
       uint32_t *stk = C.stk + g * C.stride;
       int node = 0, sp = 0;
 #ifdef IPT_BVH_STATS
@@ -969,6 +978,24 @@ __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3
                                        fmaf((float)((w0 >> 16) & 0xffu), sz, hd.z), fmaf((float)(w0 >> 24), sx, hd.x));
           const float4 b = make_float4(fmaf((float)(w1 & 0xffu), sy, hd.y), fmaf((float)((w1 >> 8) & 0xffu), sz, hd.z),
                                        ch.z, 0.f);
+#elif IPT_BVH_OCTANT
+          // lane j tests the child of rank j in the ray octant's front-to-back order
+          float4 a, b;
+          if (C.wn_lds) {  // typed per branch: ds_read_b128, not a flat load
+            const lds_f32 *pw = (const lds_f32 *)C.wn + 4 * (2 * (8 * node + oct) + 1) + 3;
+            const uint32_t sj = (__float_as_uint(*pw) >> (3 * j)) & 7u;
+            const lds_v4 *q = (const lds_v4 *)C.wn + 2 * (8 * node + (int)sj);
+            const v4f qa = q[0], qb = q[1];
+            a = make_float4(qa.x, qa.y, qa.z, qa.w);
+            b = make_float4(qb.x, qb.y, qb.z, qb.w);
+          } else {
+            const gbl_f32 *pw = (const gbl_f32 *)C.wn + 4 * (2 * (8 * node + oct) + 1) + 3;
+            const uint32_t sj = (__float_as_uint(*pw) >> (3 * j)) & 7u;
+            const gbl_v4 *q = (const gbl_v4 *)C.wn + 2 * (8 * node + (int)sj);
+            const v4f qa = q[0], qb = q[1];
+            a = make_float4(qa.x, qa.y, qa.z, qa.w);
+            b = make_float4(qb.x, qb.y, qb.z, qb.w);
+          }
 #else
           float4 a, b;
           if (C.wn_lds) {  // typed per branch: ds_read_b128, not a flat load
@@ -993,6 +1020,15 @@ __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3
           const uint32_t hm = (uint32_t)(__ballot(h) >> (lane & 56)) & 0xffu;
           if (hm == 0) {
             node = sp > 0 ? (int)stk[--sp] : kBvhDone;
+          } else if (IPT_BVH_OCTANT && !IPT_BVH_QNODES) {
+            // next = the nearest-ranked hit child; the other hits are pushed
+            // farthest first, so they pop in front-to-back order
+            const int f = __builtin_ctz(hm);
+            const int nx = __builtin_amdgcn_ds_bpermute(((lane & 56) + f) << 2, ref);
+            const uint32_t others = hm & (hm - 1u);
+            if ((others >> j) & 1u) stk[sp + __popc(others >> (j + 1))] = (uint32_t)ref;
+            sp += __popc(others);
+            node = nx;
           } else {
             float ek = h ? en : __builtin_inff();
             int rk = h ? ref : 0x7fffffff;
