@@ -846,12 +846,15 @@ __device__ __forceinline__ int closest_hit_bvh(const BvhView &B, V3 p, V3 d, flo
 #define IPT_BVH_QNODES 0
 #endif
 constexpr int kWideF4 = IPT_BVH_QNODES ? 9 : 16;  // float4 per wide node
-// IPT_BVH_OCTANT=1: lane j of a group tests the child of rank j in the ray
-// octant's precomputed front-to-back order (bvh.cpp, slot o's pad word), so
-// the next node is the lowest set bit of the hit mask -- no DPP distance
-// reduction per visit (~15 VALU), one extra dependent LDS read.
+// IPT_BVH_OCTANT=1 (default): lane j of a group tests the child of rank j in
+// the ray octant's precomputed front-to-back order (bvh.cpp, slot o's pad
+// word), so the next node is the lowest set bit of the hit mask -- no DPP
+// distance reduction per visit (~15 VALU), one extra dependent LDS read.
+// Exact either way (the visit order never changes the lexicographic result);
+// sphere scene forward 7.04 -> 6.69 ms, north-star 8.90 -> 8.57 ms
+// (profiles/r02_variants_octant.log).
 #ifndef IPT_BVH_OCTANT
-#define IPT_BVH_OCTANT 0
+#define IPT_BVH_OCTANT 1
 #endif
 struct CoopView {
   const float4 *wn;    // wide nodes (WideNode or QWideNode, kWideF4 float4 each)
