@@ -262,10 +262,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # IPT_BENCH_DEVICE / IPT_DIST_BACKEND: rehearse the N-rank path on a
+    # one-GPU box (every rank on device 0, gloo); the driver's runs use the
+    # defaults (rank i on GPU LOCAL_RANK, RCCL)
+    local = int(os.environ.get("IPT_BENCH_DEVICE", local))
+    backend = os.environ.get("IPT_DIST_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+        else:
+            dist.init_process_group(backend)
     cx = Ctx(dev, world, rank)
     b, e, rs = shard_rows_interleaved(H, world, rank)
     head = Leg(cx, CORNELL, W, H, SPP, BOUNCES, b, e, seed=args.seed, step=rs)
