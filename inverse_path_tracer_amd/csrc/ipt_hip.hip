@@ -102,6 +102,10 @@ constexpr int kMaxAdjBounces = 62;
 #define IPT_ADJU_RING 8
 #endif
 constexpr int kAdjuRing = IPT_ADJU_RING;
+// Dynamic work distribution across the waves of a launch (TraceArgs::chunk).
+#ifndef IPT_DYN_CHUNKS
+#define IPT_DYN_CHUNKS 1
+#endif
 constexpr int kMaxTableTris = 512;  // kd/kd-over-pi LDS tables up to 12 KB
 #ifndef IPT_LDS_GRAD_KB
 #define IPT_LDS_GRAD_KB 12
@@ -171,6 +175,11 @@ struct TraceArgs {
   // launch of its own kd and seed
   int nscenes, bps;
   uint64_t seed_stride, out_stride, adj_stride;
+  // dynamic work distribution (IPT_DYN_CHUNKS): a wave starts with chunk
+  // `wave` of `chunk` items and then takes chunk nwaves + atomicAdd(ctr[set])
+  // until the launch's items are used up; chunk 0 = static per-wave ranges
+  uint32_t chunk;
+  uint32_t *chunk_ctr;
 };
 
 __device__ __forceinline__ uint32_t udiv32(uint32_t n, uint64_t m, uint32_t d) {
@@ -609,8 +618,20 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   // w = lp * spp + s, or sample-major w = s * npix + lp over the launch's
   // pixels lp.  Either way the sample's seed is seed + its global index g:
   // results do not depend on the enumeration or on the row partition.
-  uint64_t next = (a.n_samples * wave) / nwaves;
-  const uint64_t end = (a.n_samples * (wave + 1)) / nwaves;
+  // Which wave traces which items only changes WHO computes a sample, never
+  // its value.  Static ranges leave the launch's tail to the waves whose
+  // pixels hold the longest paths; chunks taken from a per-launch counter
+  // keep every wave busy to the end.
+  const bool dyn = a.chunk != 0;
+  uint64_t next, end;
+  if (dyn) {
+    next = (uint64_t)wave * a.chunk;
+    end = next + a.chunk < a.n_samples ? next + a.chunk : a.n_samples;
+  } else {
+    next = (a.n_samples * wave) / nwaves;
+    end = (a.n_samples * (wave + 1)) / nwaves;
+  }
+  bool exhausted = !dyn;
 
   bool active = false;
   Rng st;
@@ -646,6 +667,18 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   int ring_n = 0, ring_h = 0;  // slots left, next slot
   const int lane = tid & 63;
   for (;;) {
+    if (next >= end && !exhausted) {  // wave-uniform: the next chunk (full exec here)
+      uint32_t c = 0;
+      if (lane == 0) c = atomicAdd(a.chunk_ctr + set, 1u);
+      c = (uint32_t)__shfl((int)c, 0);
+      const uint64_t start = (uint64_t)(nwaves + c) * a.chunk;
+      if (start < a.n_samples) {
+        next = start;
+        end = start + a.chunk < a.n_samples ? start + a.chunk : a.n_samples;
+      } else {
+        exhausted = true;
+      }
+    }
     if (RING) {
       uint64_t need = __ballot(!active);
       int n_need = __popcll(need);
@@ -1661,6 +1694,8 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   std::memcpy(a.cam, s->host.cam, sizeof a.cam);
   a.use_ring = 0;
   a.rec_cap = p.max_bounces >= 0 ? p.max_bounces + 1 : 0;
+  a.chunk = 0;
+  a.chunk_ctr = nullptr;
   a.nscenes = p.nscenes > 1 ? p.nscenes : 1;
   a.bps = 1;
   a.seed_stride = p.seed_stride;
@@ -1707,6 +1742,24 @@ static size_t table_bytes(const TraceArgs &a) {
          (a.small_pairs ? (size_t)kE3Floats * ((a.nT + 1) / 2) * sizeof(float) : 0);
 }
 
+// Per-launch scratch (the fused render's sample buffer, kd/pi of large
+// scenes) is allocated in stream order on the launch's own stream and freed
+// behind it: launches on different streams never share a buffer, and the
+// device's default pool (release threshold raised in gpu_upload) recycles
+// the blocks without a device-wide synchronisation.
+struct StreamScratch {
+  void *p = nullptr;
+  hipStream_t st = nullptr;
+  int alloc(size_t bytes, hipStream_t stream) {
+    st = stream;
+    HIP_TRY(hipMallocAsync(&p, std::max<size_t>(bytes, 16), st));
+    return 0;
+  }
+  ~StreamScratch() {
+    if (p) (void)hipFreeAsync(p, st);
+  }
+};
+
 template <int MODE, bool SPEC, bool BVH>
 static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float *kd_dev, float *out, const float *adj,
                        double *grad, const uint8_t *target, double *edges, hipStream_t st) {
@@ -1721,6 +1774,19 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
   if (a.nscenes > 1) {  // scene batch: an equal share of the resident blocks per material set
     b.bps = std::max(1, grid / a.nscenes);
     grid = b.bps * a.nscenes;
+  }
+  StreamScratch ctr;
+  b.chunk = 0;
+  b.chunk_ctr = nullptr;
+  if (IPT_DYN_CHUNKS && !(BVH && IPT_BVH_SERVER)) {
+    // ~8 chunks per wave, a multiple of 64 items, 64..4096
+    const uint64_t waves = (uint64_t)(a.nscenes > 1 ? b.bps : grid) * (kBlock / 64);
+    uint64_t c = (a.n_samples / (waves * 8) + 63) / 64 * 64;
+    c = std::min<uint64_t>(std::max<uint64_t>(c, 64), 4096);
+    b.chunk = (uint32_t)c;
+    if (ctr.alloc((size_t)a.nscenes * sizeof(uint32_t), st)) return -1;
+    HIP_TRY(hipMemsetAsync(ctr.p, 0, (size_t)a.nscenes * sizeof(uint32_t), st));
+    b.chunk_ctr = (uint32_t *)ctr.p;
   }
   hipLaunchKernelGGL((trace_kernel<MODE, SPEC, BVH>), dim3(grid), dim3(block_threads<BVH>()), lds, st, s->isect, s->pairs, s->geom,
                      s->mat, s->bnodes, s->bpairs, kd_dev ? kd_dev : s->kd, s->emit_tri, s->emit_cdf, s->emit_pmf, b,
@@ -1739,24 +1805,6 @@ __global__ __launch_bounds__(kBlock) void kdpi_kernel(const float *__restrict__ 
   const int i = blockIdx.x * kBlock + threadIdx.x;
   if (i < n) out[i] = kd[i] / kPiF;
 }
-
-// Per-launch scratch (the fused render's sample buffer, kd/pi of large
-// scenes) is allocated in stream order on the launch's own stream and freed
-// behind it: launches on different streams never share a buffer, and the
-// device's default pool (release threshold raised in gpu_upload) recycles
-// the blocks without a device-wide synchronisation.
-struct StreamScratch {
-  void *p = nullptr;
-  hipStream_t st = nullptr;
-  int alloc(size_t bytes, hipStream_t stream) {
-    st = stream;
-    HIP_TRY(hipMallocAsync(&p, std::max<size_t>(bytes, 16), st));
-    return 0;
-  }
-  ~StreamScratch() {
-    if (p) (void)hipFreeAsync(p, st);
-  }
-};
 
 template <int MODE>
 static int launch(GpuScene *s, TraceArgs a, size_t lds, const float *kd_dev, float *out, const float *adj,
