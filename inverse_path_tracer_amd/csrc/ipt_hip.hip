@@ -102,9 +102,17 @@ constexpr int kMaxAdjBounces = 62;
 #define IPT_ADJU_RING 8
 #endif
 constexpr int kAdjuRing = IPT_ADJU_RING;
-// Dynamic work distribution across the waves of a launch (TraceArgs::chunk).
+// Dynamic work distribution across the waves of a launch (TraceArgs::chunk):
+// static per-wave ranges left each launch's tail to the waves whose pixels
+// hold the longest paths -- C2 forward 2.41 -> 2.11 ms, sphere 6.61 -> 4.63 ms,
+// north-star 8.52 -> 5.79 ms, adjoints 1.16-1.63x
+// (profiles/r02_variants_dynamic_chunks.log).  IPT_DYN_CHUNKS_PER_WAVE sets
+// the chunk size (items per launch / waves / this, a multiple of 64).
 #ifndef IPT_DYN_CHUNKS
 #define IPT_DYN_CHUNKS 1
+#endif
+#ifndef IPT_DYN_CHUNKS_PER_WAVE
+#define IPT_DYN_CHUNKS_PER_WAVE 8
 #endif
 constexpr int kMaxTableTris = 512;  // kd/kd-over-pi LDS tables up to 12 KB
 #ifndef IPT_LDS_GRAD_KB
@@ -1779,9 +1787,9 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
   b.chunk = 0;
   b.chunk_ctr = nullptr;
   if (IPT_DYN_CHUNKS && !(BVH && IPT_BVH_SERVER)) {
-    // ~8 chunks per wave, a multiple of 64 items, 64..4096
+    // ~IPT_DYN_CHUNKS_PER_WAVE chunks per wave, a multiple of 64 items, 64..4096
     const uint64_t waves = (uint64_t)(a.nscenes > 1 ? b.bps : grid) * (kBlock / 64);
-    uint64_t c = (a.n_samples / (waves * 8) + 63) / 64 * 64;
+    uint64_t c = (a.n_samples / (waves * IPT_DYN_CHUNKS_PER_WAVE) + 63) / 64 * 64;
     c = std::min<uint64_t>(std::max<uint64_t>(c, 64), 4096);
     b.chunk = (uint32_t)c;
     if (ctr.alloc((size_t)a.nscenes * sizeof(uint32_t), st)) return -1;
