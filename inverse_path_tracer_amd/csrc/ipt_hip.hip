@@ -112,7 +112,7 @@ constexpr int kAdjuRing = IPT_ADJU_RING;
 #define IPT_DYN_CHUNKS 1
 #endif
 #ifndef IPT_DYN_CHUNKS_PER_WAVE
-#define IPT_DYN_CHUNKS_PER_WAVE 8
+#define IPT_DYN_CHUNKS_PER_WAVE 32
 #endif
 constexpr int kMaxTableTris = 512;  // kd/kd-over-pi LDS tables up to 12 KB
 #ifndef IPT_LDS_GRAD_KB
