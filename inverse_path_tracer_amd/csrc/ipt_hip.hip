@@ -114,6 +114,11 @@ constexpr int kAdjuRing = IPT_ADJU_RING;
 #ifndef IPT_DYN_CHUNKS_PER_WAVE
 #define IPT_DYN_CHUNKS_PER_WAVE 32
 #endif
+#ifndef IPT_DYN_SLOTS
+#define IPT_DYN_SLOTS 8
+#endif
+constexpr int kCtrSlots = IPT_DYN_SLOTS;  // chunk counters per launch (per scene set)
+constexpr int kCtrStride = 64;            // uint32 per counter: one 256-B line each
 constexpr int kMaxTableTris = 512;  // kd/kd-over-pi LDS tables up to 12 KB
 #ifndef IPT_LDS_GRAD_KB
 #define IPT_LDS_GRAD_KB 12
@@ -676,15 +681,29 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   const int lane = tid & 63;
   for (;;) {
     if (next >= end && !exhausted) {  // wave-uniform: the next chunk (full exec here)
-      uint32_t c = 0;
-      if (lane == 0) c = atomicAdd(a.chunk_ctr + set, 1u);
-      c = (uint32_t)__shfl((int)c, 0);
-      const uint64_t start = (uint64_t)(nwaves + c) * a.chunk;
-      if (start < a.n_samples) {
-        next = start;
-        end = start + a.chunk < a.n_samples ? start + a.chunk : a.n_samples;
-      } else {
-        exhausted = true;
+      // kCtrSlots counters on separate 256-B lines (one serialised address
+      // capped the grab rate near the kernel's own pace): slot k hands out
+      // chunks nwaves + c * kCtrSlots + k.  A wave draws from its home slot
+      // and, once that is used up, from the others (checked by a plain load
+      // first, so the tail costs no atomics on empty slots).
+      uint32_t *ctrs = a.chunk_ctr + (size_t)set * kCtrSlots * kCtrStride;
+      exhausted = true;
+      for (int i = 0; i < kCtrSlots; ++i) {
+        const int kk = (int)((wave + (uint32_t)i) % kCtrSlots);
+        if (i > 0) {
+          const uint32_t cur = __hip_atomic_load(ctrs + kk * kCtrStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((uint64_t)(nwaves + (uint64_t)cur * kCtrSlots + kk) * a.chunk >= a.n_samples) continue;
+        }
+        uint32_t c = 0;
+        if (lane == 0) c = atomicAdd(ctrs + kk * kCtrStride, 1u);
+        c = (uint32_t)__shfl((int)c, 0);
+        const uint64_t start = (uint64_t)(nwaves + (uint64_t)c * kCtrSlots + kk) * a.chunk;
+        if (start < a.n_samples) {
+          next = start;
+          end = start + a.chunk < a.n_samples ? start + a.chunk : a.n_samples;
+          exhausted = false;
+          break;
+        }
       }
     }
     if (RING) {
@@ -1790,10 +1809,11 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
     // ~IPT_DYN_CHUNKS_PER_WAVE chunks per wave, a multiple of 64 items, 64..4096
     const uint64_t waves = (uint64_t)(a.nscenes > 1 ? b.bps : grid) * (kBlock / 64);
     uint64_t c = (a.n_samples / (waves * IPT_DYN_CHUNKS_PER_WAVE) + 63) / 64 * 64;
-    c = std::min<uint64_t>(std::max<uint64_t>(c, 64), 4096);
+    c = std::min<uint64_t>(std::max<uint64_t>(c, 128), 4096);
     b.chunk = (uint32_t)c;
-    if (ctr.alloc((size_t)a.nscenes * sizeof(uint32_t), st)) return -1;
-    HIP_TRY(hipMemsetAsync(ctr.p, 0, (size_t)a.nscenes * sizeof(uint32_t), st));
+    const size_t bytes = (size_t)a.nscenes * kCtrSlots * kCtrStride * sizeof(uint32_t);
+    if (ctr.alloc(bytes, st)) return -1;
+    HIP_TRY(hipMemsetAsync(ctr.p, 0, bytes, st));
     b.chunk_ctr = (uint32_t *)ctr.p;
   }
   hipLaunchKernelGGL((trace_kernel<MODE, SPEC, BVH>), dim3(grid), dim3(block_threads<BVH>()), lds, st, s->isect, s->pairs, s->geom,

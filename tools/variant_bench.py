@@ -83,7 +83,8 @@ def main():
         buf = torch.empty((512 * 512 * 64, 3), device=dev)
         adj = torch.ones((512, 512, 3), device=dev)
         g = torch.zeros((8192, 3), dtype=torch.float64, device=dev)
-        kinds = ("fwd", "fsm", "adj")
+        pb = N.make_params(512, 512, 64, 4, 0, 192, 256)  # one 64-row band: a small launch (the 8-GPU share)
+        kinds = ("fwd", "fsm", "adj", "band")
         times = {n: {k: [] for k in kinds} for n in libs}
         for rnd in range(6):
             for n, L in libs.items():
@@ -97,6 +98,8 @@ def main():
                             assert L.ipt_render_samples_dev(hs[n], C.byref(p), None, buf.data_ptr(), st) == 0
                         elif kind == "fsm":
                             assert L.ipt_render_samples_sm_dev(hs[n], C.byref(p), None, buf.data_ptr(), st) == 0
+                        elif kind == "band":
+                            assert L.ipt_render_samples_sm_dev(hs[n], C.byref(pb), None, buf.data_ptr(), st) == 0
                         else:
                             assert L.ipt_adjoint_dev(hs[n], C.byref(p), None, adj.data_ptr(), g.data_ptr(), st) == 0
                     e1.record()
@@ -107,6 +110,7 @@ def main():
             f, a = np.median(times[n]["fwd"]), np.median(times[n]["adj"])
             fs = np.median(times[n]["fsm"]) if times[n]["fsm"] else float("nan")
             out[sname + ":" + n] = {"fwd_ms": round(f, 4), "fsm_ms": round(fs, 4), "adj_ms": round(a, 4),
+                                    "band_ms": round(float(np.median(times[n]["band"])), 4),
                                     "fwd_Msps": round(512 * 512 * 64 / f / 1e3, 1), "adj_Msps": round(512 * 512 * 64 / a / 1e3, 1)}
             print(sname, n, out[sname + ":" + n], flush=True)
     print(json.dumps(out))
