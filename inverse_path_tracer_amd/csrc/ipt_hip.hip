@@ -114,11 +114,9 @@ constexpr int kAdjuRing = IPT_ADJU_RING;
 #ifndef IPT_DYN_CHUNKS_PER_WAVE
 #define IPT_DYN_CHUNKS_PER_WAVE 32
 #endif
-#ifndef IPT_DYN_SLOTS
-#define IPT_DYN_SLOTS 8
+#ifndef IPT_DYN_MIN_CHUNK
+#define IPT_DYN_MIN_CHUNK 128
 #endif
-constexpr int kCtrSlots = IPT_DYN_SLOTS;  // chunk counters per launch (per scene set)
-constexpr int kCtrStride = 64;            // uint32 per counter: one 256-B line each
 constexpr int kMaxTableTris = 512;  // kd/kd-over-pi LDS tables up to 12 KB
 #ifndef IPT_LDS_GRAD_KB
 #define IPT_LDS_GRAD_KB 12
@@ -645,6 +643,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     end = (a.n_samples * (wave + 1)) / nwaves;
   }
   bool exhausted = !dyn;
+  bool pf_issued = false;  // the next chunk's atomic is in flight
+  uint32_t pf_raw = 0;     // its result (lane 0)
 
   bool active = false;
   Rng st;
@@ -680,29 +680,23 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   int ring_n = 0, ring_h = 0;  // slots left, next slot
   const int lane = tid & 63;
   for (;;) {
-    if (next >= end && !exhausted) {  // wave-uniform: the next chunk (full exec here)
-      // kCtrSlots counters on separate 256-B lines (one serialised address
-      // capped the grab rate near the kernel's own pace): slot k hands out
-      // chunks nwaves + c * kCtrSlots + k.  A wave draws from its home slot
-      // and, once that is used up, from the others (checked by a plain load
-      // first, so the tail costs no atomics on empty slots).
-      uint32_t *ctrs = a.chunk_ctr + (size_t)set * kCtrSlots * kCtrStride;
-      exhausted = true;
-      for (int i = 0; i < kCtrSlots; ++i) {
-        const int kk = (int)((wave + (uint32_t)i) % kCtrSlots);
-        if (i > 0) {
-          const uint32_t cur = __hip_atomic_load(ctrs + kk * kCtrStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((uint64_t)(nwaves + (uint64_t)cur * kCtrSlots + kk) * a.chunk >= a.n_samples) continue;
-        }
-        uint32_t c = 0;
-        if (lane == 0) c = atomicAdd(ctrs + kk * kCtrStride, 1u);
-        c = (uint32_t)__shfl((int)c, 0);
-        const uint64_t start = (uint64_t)(nwaves + (uint64_t)c * kCtrSlots + kk) * a.chunk;
+    if (dyn && !exhausted) {  // wave-uniform (full exec here)
+      // The atomic for the NEXT chunk is issued as soon as the current one is
+      // taken, so its round trip overlaps a chunk's worth of iterations
+      // instead of stalling the wave when the chunk runs out.
+      if (!pf_issued) {
+        if (lane == 0) pf_raw = atomicAdd(a.chunk_ctr + set, 1u);
+        pf_issued = true;
+      }
+      if (next >= end) {
+        const uint32_t c = (uint32_t)__shfl((int)pf_raw, 0);
+        const uint64_t start = (uint64_t)(nwaves + c) * a.chunk;
         if (start < a.n_samples) {
           next = start;
           end = start + a.chunk < a.n_samples ? start + a.chunk : a.n_samples;
-          exhausted = false;
-          break;
+          pf_issued = false;
+        } else {
+          exhausted = true;
         }
       }
     }
@@ -1809,9 +1803,9 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
     // ~IPT_DYN_CHUNKS_PER_WAVE chunks per wave, a multiple of 64 items, 64..4096
     const uint64_t waves = (uint64_t)(a.nscenes > 1 ? b.bps : grid) * (kBlock / 64);
     uint64_t c = (a.n_samples / (waves * IPT_DYN_CHUNKS_PER_WAVE) + 63) / 64 * 64;
-    c = std::min<uint64_t>(std::max<uint64_t>(c, 128), 4096);
+    c = std::min<uint64_t>(std::max<uint64_t>(c, IPT_DYN_MIN_CHUNK), 4096);
     b.chunk = (uint32_t)c;
-    const size_t bytes = (size_t)a.nscenes * kCtrSlots * kCtrStride * sizeof(uint32_t);
+    const size_t bytes = (size_t)a.nscenes * sizeof(uint32_t);
     if (ctr.alloc(bytes, st)) return -1;
     HIP_TRY(hipMemsetAsync(ctr.p, 0, bytes, st));
     b.chunk_ctr = (uint32_t *)ctr.p;
