@@ -643,8 +643,6 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     end = (a.n_samples * (wave + 1)) / nwaves;
   }
   bool exhausted = !dyn;
-  bool pf_issued = false;  // the next chunk's atomic is in flight
-  uint32_t pf_raw = 0;     // its result (lane 0)
 
   bool active = false;
   Rng st;
@@ -680,24 +678,19 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   int ring_n = 0, ring_h = 0;  // slots left, next slot
   const int lane = tid & 63;
   for (;;) {
-    if (dyn && !exhausted) {  // wave-uniform (full exec here)
-      // The atomic for the NEXT chunk is issued as soon as the current one is
-      // taken, so its round trip overlaps a chunk's worth of iterations
-      // instead of stalling the wave when the chunk runs out.
-      if (!pf_issued) {
-        if (lane == 0) pf_raw = atomicAdd(a.chunk_ctr + set, 1u);
-        pf_issued = true;
-      }
-      if (next >= end) {
-        const uint32_t c = (uint32_t)__shfl((int)pf_raw, 0);
-        const uint64_t start = (uint64_t)(nwaves + c) * a.chunk;
-        if (start < a.n_samples) {
-          next = start;
-          end = start + a.chunk < a.n_samples ? start + a.chunk : a.n_samples;
-          pf_issued = false;
-        } else {
-          exhausted = true;
-        }
+    if (next >= end && !exhausted) {  // wave-uniform: the next chunk (full exec here)
+      // One counter, grabbed when needed.  Measured against alternatives
+      // (profiles/r02_variants_chunk_*.log): 8 counters on separate lines
+      // with stealing and a grab prefetched one chunk ahead were both slower.
+      uint32_t c = 0;
+      if (lane == 0) c = atomicAdd(a.chunk_ctr + set, 1u);
+      c = (uint32_t)__shfl((int)c, 0);
+      const uint64_t start = (uint64_t)(nwaves + c) * a.chunk;
+      if (start < a.n_samples) {
+        next = start;
+        end = start + a.chunk < a.n_samples ? start + a.chunk : a.n_samples;
+      } else {
+        exhausted = true;
       }
     }
     if (RING) {
