@@ -179,7 +179,11 @@ struct TraceArgs {
   float rc_spp;
   int use_ring;  // RING instances: camera rays from the LDS ring (host decides: only if it costs no residency)
   int rec_cap;   // ADJ: vertex records per lane (max_bounces + 1); ADJU: ring slots
-  // scene batch (C5): blocks [b * bps, (b+1) * bps) trace material set b --
+  // scene batch (C5): blocks b, b + nscenes, ... (bps of them) trace material
+  // set b -- interleaved, not contiguous ranges: the dispatcher fills a CU
+  // with consecutive workgroups, so contiguous ranges gave some sets fewer
+  // CUs and the launch waited on them (C5 forward 5.77 -> 4.81 ms, adjoint
+  // 6.66 -> 5.29 ms, profiles/r02_batch_interleave.log) --
   // kd + b*3nT, seed + b*seed_stride, outputs at b * (out|adj)_stride,
   // gradient at b*3nT -- so each workgroup holds ONE set's tables and bins
   // (the single-scene LDS footprint) and every set is the single-scene
@@ -478,8 +482,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   extern __shared__ double lds[];
   const int tid = threadIdx.x;
   // scene batch: this workgroup's material set and its place among the set's blocks
-  const int set = a.nscenes > 1 ? (int)(blockIdx.x / (uint32_t)a.bps) : 0;
-  const uint32_t sblock = blockIdx.x - (uint32_t)set * (uint32_t)(a.nscenes > 1 ? a.bps : 0);
+  const int set = a.nscenes > 1 ? (int)(blockIdx.x % (uint32_t)a.nscenes) : 0;
+  const uint32_t sblock = a.nscenes > 1 ? blockIdx.x / (uint32_t)a.nscenes : blockIdx.x;
   const uint32_t sgrid = a.nscenes > 1 ? (uint32_t)a.bps : gridDim.x;
   const uint64_t seed = a.seed + (uint64_t)set * a.seed_stride;
   if (a.nscenes > 1) {

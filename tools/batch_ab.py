@@ -48,15 +48,50 @@ def main():
             q = N.make_params(W, H, spp, mb, b * W * H * spp)
             N.check(L.ipt_adjoint_dev(sc.handle, C.byref(q), kd[b].data_ptr(), adj[b].data_ptr(), g[b].data_ptr(), st))
 
+    p416 = N.make_params(W, H, spp * S, mb, 0)
+    p512 = N.make_params(512, 512, 64, mb, 0)
+    o512 = torch.empty((512, 512, 3), device="cuda")
+    a512 = torch.ones((512, 512, 3), device="cuda")
+
+    def deep_fwd():
+        N.check(L.ipt_render_dev(sc.handle, C.byref(p416), kd[0].data_ptr(), hdr[0].data_ptr(), None, st))
+
+    def deep_adj():
+        N.check(L.ipt_adjoint_dev(sc.handle, C.byref(p416), kd[0].data_ptr(), adj[0].data_ptr(), g[0].data_ptr(), st))
+
+    def c3_fwd():
+        N.check(L.ipt_render_dev(sc.handle, C.byref(p512), kd[0].data_ptr(), o512.data_ptr(), None, st))
+
+    def c3_adj():
+        N.check(L.ipt_adjoint_dev(sc.handle, C.byref(p512), kd[0].data_ptr(), a512.data_ptr(), g[0].data_ptr(), st))
+
     def tall_fwd():
         N.check(L.ipt_render_dev(sc.handle, C.byref(pbig), kd[0].data_ptr(), big.data_ptr(), None, st))
 
     def tall_adj():
         N.check(L.ipt_adjoint_dev(sc.handle, C.byref(pbig), kd[0].data_ptr(), adjbig.data_ptr(), g[0].data_ptr(), st))
 
+    def batch_s(nsets, sppx, same_kd=False):
+        q = N.make_params(W, H, sppx, mb, 0)
+        k = kd[:1].expand(nsets, -1, -1).contiguous() if same_kd else kd[:nsets].contiguous()
+        def f():
+            N.check(L.ipt_render_batch_dev(sc.handle, C.byref(q), nsets, W * H * sppx, k.data_ptr(), hdr.data_ptr(), st))
+        def b():
+            N.check(L.ipt_adjoint_batch_dev(sc.handle, C.byref(q), nsets, W * H * sppx, k.data_ptr(), adj.data_ptr(),
+                                            g.data_ptr(), st))
+        return f, b
+
+    extra = []
+    for nsets, sppx in [(1, 416), (2, 208), (4, 104), (8, 52)]:
+        f, b = batch_s(nsets, sppx)
+        extra += [("batch%d_fwd" % nsets, f), ("batch%d_adj" % nsets, b)]
+    f, b = batch_s(13, 32, True)
+    extra += [("batch13same_fwd", f), ("batch13same_adj", b)]
     out = {}
     for name, fn in [("batch_fwd", batch_fwd), ("singles_fwd", singles_fwd), ("tall_fwd", tall_fwd),
-                     ("batch_adj", batch_adj), ("singles_adj", singles_adj), ("tall_adj", tall_adj)]:
+                     ("deep_fwd", deep_fwd), ("c3_fwd_16.8M", c3_fwd),
+                     ("batch_adj", batch_adj), ("singles_adj", singles_adj), ("tall_adj", tall_adj),
+                     ("deep_adj", deep_adj), ("c3_adj_16.8M", c3_adj)] + extra:
         fn()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
