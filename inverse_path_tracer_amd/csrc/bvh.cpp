@@ -288,6 +288,39 @@ int acceptance_box(const TriIsect &T, const TriGeom &G, double r_all, float lo[3
   return 0;
 }
 
+std::vector<PairBox2> pair_boxes(const HostScene &S) {
+  const float inf = std::numeric_limits<float>::infinity();
+  const int nP = (S.nT + 1) / 2;
+  std::vector<PairBox2> out((size_t)(nP + 1) / 2);
+  const double r_all = scene_coord_bound(S);
+  for (int j = 0; j < nP; ++j) {
+    float lo[3] = {inf, inf, inf}, hi[3] = {-inf, -inf, -inf};
+    bool any = false, unbounded = false;
+    for (int h = 0; h < 2; ++h) {
+      const int i = 2 * j + h;
+      if (i >= S.nT) continue;  // the padding triangle is never accepted
+      float l[3], u[3];
+      const int rc = acceptance_box(S.isect[(size_t)i], S.geom[(size_t)i], r_all, l, u);
+      if (rc < 0) unbounded = true;
+      if (rc != 0) continue;
+      any = true;
+      for (int a = 0; a < 3; ++a) {
+        lo[a] = std::min(lo[a], l[a]);
+        hi[a] = std::max(hi[a], u[a]);
+      }
+    }
+    float b[6];
+    for (int a = 0; a < 3; ++a) {
+      b[2 * a] = unbounded ? -inf : (any ? lo[a] : inf);
+      b[2 * a + 1] = unbounded ? inf : (any ? hi[a] : inf);
+    }
+    for (int k = 0; k < 6; ++k) out[(size_t)j / 2].f[k][j & 1] = b[k];
+  }
+  if (nP & 1)  // the record's unused half: never tested (the loop stops at nP)
+    for (int k = 0; k < 6; ++k) out.back().f[k][1] = inf;
+  return out;
+}
+
 // Collapse the binary tree into 8-wide nodes: starting from a binary node's
 // two children, repeatedly open the inner child with the largest box until
 // the node has 8 children or only leaves remain.  Leaves keep their binary

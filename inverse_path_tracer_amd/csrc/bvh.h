@@ -25,4 +25,9 @@ int acceptance_box(const TriIsect &T, const TriGeom &G, double r_all, float lo[3
 // |camera origin|, plus one).
 double scene_coord_bound(const HostScene &S);
 
+// Acceptance boxes of the brute-force pair loop's pairs (2j, 2j+1), two pairs
+// per record (scene_layout.h PairBox2), for the culled shadow cast of small
+// scenes (ipt_device.h::shadow_hit_pairs_small).
+std::vector<PairBox2> pair_boxes(const HostScene &S);
+
 }  // namespace ipt

@@ -450,6 +450,36 @@ __device__ __forceinline__ void pair_ray(const TriPair &T, const PairOrigin &o, 
   bt = tb ? t.y : bt;
   bi = tb ? ib : bi;
 }
+// pair_ray's arithmetic reduced to "does either triangle accept with t below
+// its bound" (ba for the first, bb for the second) -- the culled shadow cast.
+__device__ __forceinline__ bool pair_occludes(const TriPair &T, const PairOrigin &o, float ba, float bb, V3 p, V3 d,
+                                              f2 e03, f2 e13, f2 e23) {
+  const f2 n0 = ld2(T, 3), n1 = ld2(T, 4), n2 = ld2(T, 5);
+  const f2 denom = fma2(n2, bc2(d.z), fma2(n1, bc2(d.y), n0 * bc2(d.x)));
+  const f2 num = o.num;
+#if IPT_FASTDIV
+  const f2 nb = denom;
+  const f2 r0 = f2{__builtin_amdgcn_rcpf(-denom.x), __builtin_amdgcn_rcpf(-denom.y)};
+  const f2 e0 = fma2(nb, r0, bc2(1.0f));
+  const f2 r1 = fma2(e0, r0, r0);
+  const f2 q0 = num * r1;
+  const f2 e1 = fma2(nb, q0, num);
+  const f2 q1 = fma2(e1, r1, q0);
+  const f2 e2 = fma2(nb, q1, num);
+  const f2 t = fma2(e2, r1, q1);  // == div_inrange(num, -denom) per half
+#else
+  const f2 t = f2{num.x / -denom.x, num.y / -denom.y};
+#endif
+  const f2 qx = fma2(bc2(d.x), t, bc2(p.x)), qy = fma2(bc2(d.y), t, bc2(p.y)), qz = fma2(bc2(d.z), t, bc2(p.z));
+  const f2 s0 = fma2(qz, ld2(T, 8), fma2(qy, ld2(T, 7), fma2(qx, ld2(T, 6), e03)));
+  const f2 s1 = fma2(qz, ld2(T, 12), fma2(qy, ld2(T, 11), fma2(qx, ld2(T, 10), e13)));
+  const f2 s2 = fma2(qz, ld2(T, 16), fma2(qy, ld2(T, 15), fma2(qx, ld2(T, 14), e23)));
+  const bool oa = !(fabsf(denom.x) < kMinDotUp) && !(t.x < kEpsUp) && (t.x < ba) && !(s0.x > 0.f) &&
+                  !(s1.x > 0.f) && !(s2.x > 0.f);
+  const bool ob = !(fabsf(denom.y) < kMinDotUp) && !(t.y < kEpsUp) && (t.y < bb) && !(s0.y > 0.f) &&
+                  !(s1.y > 0.f) && !(s2.y > 0.f);
+  return oa | ob;
+}
 __device__ __forceinline__ void hit_test_pair(const TriPair &T, int i, V3 p, V3 d, float &bt, int &bi) {
   pair_ray(T, pair_origin(T, p), i, i + 1, p, d, bt, bi, ld2(T, 9), ld2(T, 13), ld2(T, 17));
 }
@@ -575,7 +605,7 @@ constexpr int kBvhDone = (int)0x80000000;
 // triangle tests, [5] coop calls with >= 1 ray (per wave), [6] coop rounds
 // (per wave); pre-pass: [7] casts, [8] large-triangle tests, [9] shadow
 // target tests, [10] shadow rays decided before the tree.
-constexpr int kBvhStats = 12;
+constexpr int kBvhStats = 16;  // [12..15]: culled shadow casts (shadow_hit_pairs_small)
 #ifdef IPT_BVH_STATS
 __device__ unsigned long long g_bvh_stats[kBvhStats];
 #endif
@@ -686,6 +716,103 @@ __device__ __forceinline__ SlabRay slab_ray(V3 p, V3 d) {
   const float oz = fabsf(d.z) < 0x1p-60f ? qnan : -(p.z * iz);
   return SlabRay{bc2(ix), bc2(iy), bc2(iz), bc2(ox), bc2(oy), bc2(oz)};
 }
+// Shadow ray of the small-scene loop (closest_hit_pairs_small's scenes)
+// towards emitter triangle `target`, with pair culling.  Only `result ==
+// target` and then t are used by the caller, so: (1) the target is tested
+// first (a miss decides the lane); (2) the pairs are then visited in index
+// order keeping the lexicographic minimum of (t, index) -- the same hit as the
+// in-order strict '<' loop whatever is skipped, as long as no skipped pair
+// could be accepted with t <= bt (bvh.cpp, BVH traversal); (3) a pair is
+// skipped for the whole wave when no live lane's ray enters its acceptance
+// box (PairBox2) within [kEpsUp, bt].  The lower bound is kEpsUp, not 0: the
+// test rejects t < kEpsUp, and bvh.cpp's padding keeps the computed t of
+// every acceptable hit inside the computed [entry, exit].  A shadow ray
+// starts ON its vertex's wall, inside that wall's thin box, but leaves it
+// long before t = 1e-2 unless it grazes the wall; all rays of a wave head for
+// the light, so most pairs are skipped for every lane.  A lane is done as
+// soon as the best hit is not the target (occluded).
+#ifndef IPT_SHADOW_CULL
+#define IPT_SHADOW_CULL 1
+#endif
+__device__ __forceinline__ int shadow_hit_pairs_small(const TriIsect *__restrict__ isect,
+                                                      const TriPair *__restrict__ pairs,
+                                                      const PairBox2 *__restrict__ boxes, const f2 *e3, int nT, V3 p,
+                                                      V3 d, int target, float &best_t) {
+  float bt = __builtin_inff();
+  int bi = -1;
+  hit_test(isect[target], target, p, d, bt, bi);
+  bool live = bi >= 0;
+  int nP = (nT + 1) >> 1;
+  asm volatile("" : "+s"(nP));
+  typedef __attribute__((address_space(3))) const f2 lds_f2;
+  lds_f2 *e3l = (lds_f2 *)e3;
+  if (IPT_PIN_E3) asm volatile("" : "+v"(e3l));
+#ifdef IPT_BVH_STATS
+  atomicAdd(&g_bvh_stats[12], 1ull);                      // shadow lanes
+  if (live) atomicAdd(&g_bvh_stats[13], 1ull);            // ... whose target is accepted
+  if (__lane_id() == __ffsll((unsigned long long)__builtin_amdgcn_ballot_w64(true)) - 1)
+    atomicAdd(&g_bvh_stats[14], 1ull);                    // wave-level calls
+#endif
+  // opaque per cast: the compiler would otherwise hoist the loop-invariant
+  // box loads out of the megakernel loop into SGPRs, which then spill
+  asm volatile("" : "+s"(boxes));
+  if (__builtin_amdgcn_ballot_w64(live)) {
+    // (a) this lane's candidate pairs: bit j = its ray enters pair j's box
+    // within [kEpsUp, bt] (computed first, so that the slab registers are
+    // dead before the pair tests)
+    uint32_t need = 0;
+    {
+      const SlabRay r = slab_ray(p, d);
+#pragma unroll
+      for (int J = 0; J < kSmallPairs / 2; ++J) {
+        if (2 * J < nP) {  // wave-uniform
+          const PairBox2 B = boxes[J];
+          const f2 tx0 = fma2(f2{B.f[0][0], B.f[0][1]}, r.ix, r.ox), tx1 = fma2(f2{B.f[1][0], B.f[1][1]}, r.ix, r.ox);
+          const f2 ty0 = fma2(f2{B.f[2][0], B.f[2][1]}, r.iy, r.oy), ty1 = fma2(f2{B.f[3][0], B.f[3][1]}, r.iy, r.oy);
+          const f2 tz0 = fma2(f2{B.f[4][0], B.f[4][1]}, r.iz, r.oz), tz1 = fma2(f2{B.f[5][0], B.f[5][1]}, r.iz, r.oz);
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const float en = fmaxf(fmaxf(fminf(tx0[h], tx1[h]), fminf(ty0[h], ty1[h])),
+                                   fmaxf(fminf(tz0[h], tz1[h]), kEpsUp));
+            const float ex = fminf(fminf(fmaxf(tx0[h], tx1[h]), fmaxf(ty0[h], ty1[h])),
+                                   fminf(fmaxf(tz0[h], tz1[h]), bt));
+            need |= (en <= ex ? 1u : 0u) << (2 * J + h);
+          }
+        }
+      }
+    }
+    // (b) the pairs some live lane needs, in index order.  Only "is the
+    // target still the lexicographic minimum" matters, so bt stays t_e: pair
+    // triangle i occludes iff it is accepted with t < t_e, or t == t_e and
+    // i < target, i.e. t < bound_i with bound_i = nextup(t_e) for i < target
+    // (t_e >= kEpsUp > 0 is finite: +1 on the bits is nextup).
+    const float te = bt, teu = __uint_as_float(__float_as_uint(bt) + 1u);
+#pragma unroll
+    for (int j = 0; j < kSmallPairs; ++j) {
+      if (j < nP) {  // wave-uniform
+        if (__builtin_amdgcn_ballot_w64(live && ((need >> j) & 1u))) {
+#ifdef IPT_BVH_STATS
+          if (__lane_id() == __ffsll((unsigned long long)__builtin_amdgcn_ballot_w64(true)) - 1)
+            atomicAdd(&g_bvh_stats[15], 1ull);                // wave-level pair tests
+#endif
+          if (live) {
+            const TriPair T = pairs[j];
+            const bool occ = pair_occludes(T, pair_origin(T, p), 2 * j < target ? teu : te,
+                                           2 * j + 1 < target ? teu : te, p, d, e3l[3 * j], e3l[3 * j + 1],
+                                           e3l[3 * j + 2]);
+            if (occ) {
+              live = false;
+              bi = -1;  // not the target (the caller only compares with it)
+            }
+          }
+        }
+      }
+    }
+  }
+  best_t = bt;
+  return bi;
+}
+
 // Both children's boxes of an inner node against [0, bt]: h0/h1 = hit,
 // en0/en1 = entry parameters, c0/c1 = child links.
 __device__ __forceinline__ void bvh_node_test(const BvhView &B, int node, const SlabRay &r, float bt, bool &h0,

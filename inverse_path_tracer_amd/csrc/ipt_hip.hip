@@ -36,6 +36,7 @@
 #include <string>
 #include <vector>
 
+#include "bvh.h"
 #include "gpu_api.h"
 #include "ipt_device.h"
 
@@ -195,6 +196,8 @@ struct TraceArgs {
   // until the launch's items are used up; chunk 0 = static per-wave ranges
   uint32_t chunk;
   uint32_t *chunk_ctr;
+  // small scenes: acceptance boxes of the pairs (culled shadow casts)
+  const PairBox2 *pboxes;
 };
 
 __device__ __forceinline__ uint32_t udiv32(uint32_t n, uint64_t m, uint32_t d) {
@@ -337,10 +340,13 @@ constexpr int min_blocks() {
 #ifndef IPT_RAY_RING
 #define IPT_RAY_RING 1
 #endif
+#ifndef IPT_RAY_RING_FWD
+#define IPT_RAY_RING_FWD 0
+#endif
 constexpr int kRingFields = 9;  // d.xyz, XORWOW d, v0..v4
 template <int MODE, bool BVH>
 constexpr bool ring_on() {
-  return IPT_RAY_RING && !BVH && MODE == 1;
+  return IPT_RAY_RING && !BVH && (MODE == 1 || (IPT_RAY_RING_FWD && MODE == 0));
 }
 // Work enumeration of the adjoint and graph integrators.  Sample-major (1):
 // a wave's 64 lanes trace 64 different pixels, so their paths diverge at once
@@ -946,7 +952,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         if (shadow && bvh_prepass<true>(bv, p, sd, ts, hs, et)) qn = coop_root_test(cv, p, sd, ts);
         coop_cast<true>(cv, qn, p, sd, ts, hs);
       } else if (!SERVE && shadow) {
-        hs = cast<BVH>(isect, pairs, e3, nT, bv, p, sd, ts, et);
+        if (!BVH && IPT_SHADOW_CULL && e3)
+          hs = shadow_hit_pairs_small(isect, pairs, a.pboxes, e3, nT, p, sd, et, ts);
+        else
+          hs = cast<BVH>(isect, pairs, e3, nT, bv, p, sd, ts, et);
       }
       PHASE(3)
       if (shadow && hs == et) {  // must hit the sampled emitter itself
@@ -1478,6 +1487,7 @@ struct GpuScene {
   int32_t *big_idx = nullptr;
   float4 *wide = nullptr;  // WideNode or QWideNode records (IPT_BVH_QNODES)
   TriIsect *wtris = nullptr;
+  PairBox2 *pboxes = nullptr;  // pair acceptance boxes (small scenes' culled shadow casts)
   int accel = IPT_ACCEL_AUTO;
   int *grad_map = nullptr, *slot_tri = nullptr;  // ADJ hot-set LDS slots (large scenes)
   int grid[16] = {0};       // resident workgroups per (mode, spec, bvh) (0 = not queried)
@@ -1535,7 +1545,7 @@ GpuScene *gpu_upload(const HostScene &host, std::string *err) {
       upload(&s->emit_pmf, host.emit_pmf) || upload(&s->bnodes, host.bvh_nodes) || upload(&s->bpairs, host.bvh_pairs) ||
       upload(&s->big_pairs, host.bvh_big_pairs) || upload(&s->big_idx, host.bvh_big_idx) ||
       (IPT_BVH_QNODES ? upload_as_f4(&s->wide, host.bvh_qwide) : upload_as_f4(&s->wide, host.bvh_wide)) ||
-      upload(&s->wtris, host.bvh_wtris)) {
+      upload(&s->wtris, host.bvh_wtris) || upload(&s->pboxes, pair_boxes(host))) {
     *err = gpu_last_error();
     gpu_free(s);
     return nullptr;
@@ -1597,6 +1607,7 @@ void gpu_free(GpuScene *s) {
   (void)hipFree(s->big_idx);
   (void)hipFree(s->wide);
   (void)hipFree(s->wtris);
+  (void)hipFree(s->pboxes);
   (void)hipFree(s->grad_map);
   (void)hipFree(s->slot_tri);
   delete s;
@@ -1714,6 +1725,7 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.rec_cap = p.max_bounces >= 0 ? p.max_bounces + 1 : 0;
   a.chunk = 0;
   a.chunk_ctr = nullptr;
+  a.pboxes = s->pboxes;
   a.nscenes = p.nscenes > 1 ? p.nscenes : 1;
   a.bps = 1;
   a.seed_stride = p.seed_stride;

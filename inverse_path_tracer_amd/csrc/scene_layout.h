@@ -146,6 +146,17 @@ struct QWideNode {
 };
 static_assert(sizeof(QWideNode) == 144, "QWideNode layout");
 
+// Acceptance boxes (bvh.cpp) of the brute-force loop's triangle pairs, two
+// pairs per record so one packed fma computes a slab parameter of both:
+// f[k] = {pair 2J, pair 2J+1}, k = lo.x hi.x lo.y hi.y lo.z hi.z.  A pair's
+// box is the union of its triangles' boxes; a triangle without a bounded
+// acceptance region makes its pair's box infinite (never culled); a pair
+// that can never be accepted gets {+inf, +inf} per axis (always culled).
+struct PairBox2 {
+  float f[6][2];
+};
+static_assert(sizeof(PairBox2) == 48, "PairBox2 layout");
+
 // Device view of a loaded scene (all pointers are device pointers).
 struct DevScene {
   int nT, nE;

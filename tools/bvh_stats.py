@@ -29,7 +29,8 @@ from inverse_path_tracer_amd import _native as N  # noqa: E402
 from inverse_path_tracer_amd.scene import ObjectSpec, Scene  # noqa: E402
 
 NAMES = ["tree_rays", "node_visits", "leaf_visits", "shadow_occluded_in_tree", "leaf_tri_tests", "coop_calls",
-         "coop_rounds", "casts", "prepass_tri_tests", "shadow_target_tests", "shadow_decided_before_tree", "unused"]
+         "coop_rounds", "casts", "prepass_tri_tests", "shadow_target_tests", "shadow_decided_before_tree", "unused",
+         "cull_shadow_lanes", "cull_target_accepted", "cull_wave_calls", "cull_wave_pair_tests"]
 
 
 def derive(c, n):
@@ -42,7 +43,10 @@ def derive(c, n):
             "nodes_per_tree_ray": c["node_visits"] / max(1, c["tree_rays"]),
             "leaf_tris_per_tree_ray": c["leaf_tri_tests"] / max(1, c["tree_rays"]),
             "rays_per_coop_round": c["tree_rays"] / max(1, c["coop_rounds"]),
-            "rounds_per_coop_call": c["coop_rounds"] / max(1, c["coop_calls"])}
+            "rounds_per_coop_call": c["coop_rounds"] / max(1, c["coop_calls"]),
+            "cull_target_accepted_frac": c["cull_target_accepted"] / max(1, c["cull_shadow_lanes"]),
+            "cull_lanes_per_wave_call": c["cull_shadow_lanes"] / max(1, c["cull_wave_calls"]),
+            "cull_pairs_tested_per_wave_call": c["cull_wave_pair_tests"] / max(1, c["cull_wave_calls"])}
 
 
 def main():

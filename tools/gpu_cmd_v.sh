@@ -1,0 +1,6 @@
+# variant A/B only (VARIANTS), scenes per IPT_VB_* env
+set -o pipefail
+R=$GRAFT_REPO_ROOT; OUT=$R/gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp; cd $R
+T=${TAG:-v}
+timeout -k 10 400 python tools/variant_bench.py ${VARIANTS:-base} > $OUT/variants_$T.log 2>&1
+echo "rc=$?"

@@ -1,0 +1,7 @@
+# GPU parity tests, then a variant A/B (VARIANTS) in one call
+set -o pipefail
+R=$GRAFT_REPO_ROOT; OUT=$R/gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp; cd $R
+T=${TAG:-vt}
+timeout -k 10 600 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest_$T.log 2>&1 &&
+timeout -k 10 400 python tools/variant_bench.py ${VARIANTS:-base} > $OUT/variants_$T.log 2>&1
+echo "rc=$?"
