@@ -766,10 +766,10 @@ __device__ __forceinline__ int shadow_hit_pairs_small(const TriIsect *__restrict
 #pragma unroll
       for (int J = 0; J < kSmallPairs / 2; ++J) {
         if (2 * J < nP) {  // wave-uniform
-          const PairBox2 B = boxes[J];
-          const f2 tx0 = fma2(f2{B.f[0][0], B.f[0][1]}, r.ix, r.ox), tx1 = fma2(f2{B.f[1][0], B.f[1][1]}, r.ix, r.ox);
-          const f2 ty0 = fma2(f2{B.f[2][0], B.f[2][1]}, r.iy, r.oy), ty1 = fma2(f2{B.f[3][0], B.f[3][1]}, r.iy, r.oy);
-          const f2 tz0 = fma2(f2{B.f[4][0], B.f[4][1]}, r.iz, r.oz), tz1 = fma2(f2{B.f[5][0], B.f[5][1]}, r.iz, r.oz);
+          const cst_f32 *B = (const cst_f32 *)(boxes + J);  // scalar loads
+          const f2 tx0 = fma2(f2{B[0], B[1]}, r.ix, r.ox), tx1 = fma2(f2{B[2], B[3]}, r.ix, r.ox);
+          const f2 ty0 = fma2(f2{B[4], B[5]}, r.iy, r.oy), ty1 = fma2(f2{B[6], B[7]}, r.iy, r.oy);
+          const f2 tz0 = fma2(f2{B[8], B[9]}, r.iz, r.oz), tz1 = fma2(f2{B[10], B[11]}, r.iz, r.oz);
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const float en = fmaxf(fmaxf(fminf(tx0[h], tx1[h]), fminf(ty0[h], ty1[h])),

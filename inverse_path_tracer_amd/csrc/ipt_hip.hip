@@ -274,14 +274,17 @@ __device__ __forceinline__ void item_ray(const TraceArgs &a, uint64_t seed, uint
 
 // ---------------------------------------------------------------------------
 // Minimum resident 256-thread blocks per CU (= waves per SIMD) requested per
-// integrator; 0 lets the compiler choose.  Measured (profiles/
-// r01_variants_*.log): 6 for the forward (80 VGPRs, 20 B of cold spill) and
-// the adjoint (80 VGPRs; its LDS records fit 6 blocks) beat 5 and natural.
+// integrator; 0 lets the compiler choose.  Round 1 measured 6 best (80 VGPRs,
+// 20 B of cold spill); with the dynamic chunks, the culled shadow cast and
+// the batch fields the 80-VGPR build spills 72-76 B per lane inside the loop
+// and 5 (96 VGPRs, 12-20 B) wins: C2 forward 2.11 -> 1.98 ms, adjoint 2.49 ->
+// 2.41, scenes/0 2.66 -> 2.53 / 2.98 -> 2.95; 4 (108-115 VGPRs, no spill)
+// loses (profiles/r02_variants_occupancy.log).
 #ifndef IPT_MIN_BLOCKS_FWD
-#define IPT_MIN_BLOCKS_FWD 6
+#define IPT_MIN_BLOCKS_FWD 5
 #endif
 #ifndef IPT_MIN_BLOCKS_ADJ
-#define IPT_MIN_BLOCKS_ADJ 6
+#define IPT_MIN_BLOCKS_ADJ 5
 #endif
 #ifndef IPT_MIN_BLOCKS_GRAPH
 #define IPT_MIN_BLOCKS_GRAPH 0
