@@ -605,7 +605,7 @@ constexpr int kBvhDone = (int)0x80000000;
 // triangle tests, [5] coop calls with >= 1 ray (per wave), [6] coop rounds
 // (per wave); pre-pass: [7] casts, [8] large-triangle tests, [9] shadow
 // target tests, [10] shadow rays decided before the tree.
-constexpr int kBvhStats = 16;  // [12..15]: culled shadow casts (shadow_hit_pairs_small)
+constexpr int kBvhStats = 18;  // [12..17]: culled shadow casts (shadow_hit_pairs_small)
 #ifdef IPT_BVH_STATS
 __device__ unsigned long long g_bvh_stats[kBvhStats];
 #endif
@@ -750,6 +750,7 @@ __device__ __forceinline__ int shadow_hit_pairs_small(const TriIsect *__restrict
 #ifdef IPT_BVH_STATS
   atomicAdd(&g_bvh_stats[12], 1ull);                      // shadow lanes
   if (live) atomicAdd(&g_bvh_stats[13], 1ull);            // ... whose target is accepted
+  if (live) atomicAdd(&g_bvh_stats[17], (unsigned long long)nP);  // lane box tests
   if (__lane_id() == __ffsll((unsigned long long)__builtin_amdgcn_ballot_w64(true)) - 1)
     atomicAdd(&g_bvh_stats[14], 1ull);                    // wave-level calls
 #endif
@@ -796,6 +797,9 @@ __device__ __forceinline__ int shadow_hit_pairs_small(const TriIsect *__restrict
             atomicAdd(&g_bvh_stats[15], 1ull);                // wave-level pair tests
 #endif
           if (live) {
+#ifdef IPT_BVH_STATS
+            atomicAdd(&g_bvh_stats[16], 1ull);                // lane pair tests
+#endif
             const TriPair T = pairs[j];
             const bool occ = pair_occludes(T, pair_origin(T, p), 2 * j < target ? teu : te,
                                            2 * j + 1 < target ? teu : te, p, d, e3l[3 * j], e3l[3 * j + 1],

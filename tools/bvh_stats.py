@@ -30,7 +30,8 @@ from inverse_path_tracer_amd.scene import ObjectSpec, Scene  # noqa: E402
 
 NAMES = ["tree_rays", "node_visits", "leaf_visits", "shadow_occluded_in_tree", "leaf_tri_tests", "coop_calls",
          "coop_rounds", "casts", "prepass_tri_tests", "shadow_target_tests", "shadow_decided_before_tree", "unused",
-         "cull_shadow_lanes", "cull_target_accepted", "cull_wave_calls", "cull_wave_pair_tests"]
+         "cull_shadow_lanes", "cull_target_accepted", "cull_wave_calls", "cull_wave_pair_tests",
+         "cull_lane_pair_tests", "cull_lane_box_tests"]
 
 
 def derive(c, n):
@@ -46,12 +47,15 @@ def derive(c, n):
             "rounds_per_coop_call": c["coop_rounds"] / max(1, c["coop_calls"]),
             "cull_target_accepted_frac": c["cull_target_accepted"] / max(1, c["cull_shadow_lanes"]),
             "cull_lanes_per_wave_call": c["cull_shadow_lanes"] / max(1, c["cull_wave_calls"]),
-            "cull_pairs_tested_per_wave_call": c["cull_wave_pair_tests"] / max(1, c["cull_wave_calls"])}
+            "cull_pairs_tested_per_wave_call": c["cull_wave_pair_tests"] / max(1, c["cull_wave_calls"]),
+            "cull_shadow_casts_per_sample": c["cull_shadow_lanes"] / n,
+            "cull_tri_tests_per_sample": (c["cull_shadow_lanes"] + 2 * c["cull_lane_pair_tests"]) / n,
+            "cull_box_tests_per_sample": c["cull_lane_box_tests"] / n}
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--scenes", default="northstar,sphere")
+    ap.add_argument("--scenes", default="northstar,sphere,cornell,scene0")
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--bounces", type=int, default=4)
