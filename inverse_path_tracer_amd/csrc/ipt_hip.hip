@@ -199,6 +199,7 @@ struct TraceArgs {
   // small scenes: acceptance boxes of the pairs (culled shadow casts)
   const PairBox2 *pboxes;
 };
+static_assert(alignof(TraceArgs) == 8, "TraceArgs sits right after the ten 8-B scene pointers in the kernarg segment");
 
 __device__ __forceinline__ uint32_t udiv32(uint32_t n, uint64_t m, uint32_t d) {
   return d == 1u ? n : (uint32_t)__umul64hi(m, (uint64_t)n);
@@ -346,6 +347,12 @@ constexpr int min_blocks() {
 #ifndef IPT_RAY_RING_FWD
 #define IPT_RAY_RING_FWD 0
 #endif
+// trace_kernel re-reads its TraceArgs from the kernarg segment each loop
+// iteration (see the loop head).  Offset: the ten scene pointers before it.
+#ifndef IPT_ARGS_RELOAD
+#define IPT_ARGS_RELOAD 1
+#endif
+[[maybe_unused]] constexpr size_t kTraceArgsOffset = 10 * sizeof(void *);
 constexpr int kRingFields = 9;  // d.xyz, XORWOW d, v0..v4
 template <int MODE, bool BVH>
 constexpr bool ring_on() {
@@ -691,6 +698,19 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   int ring_n = 0, ring_h = 0;  // slots left, next slot
   const int lane = tid & 63;
   for (;;) {
+#if IPT_ARGS_RELOAD && defined(__HIP_DEVICE_COMPILE__)  // (the host pass has no AS4 copy)
+    // The launch arguments, re-read from the kernarg segment every iteration
+    // through a pointer the compiler cannot see through: left alone it keeps
+    // the loop-invariant fields (camera, divisors, pointers) in SGPRs for
+    // the whole loop, runs out of them and spills them to VGPR lanes, paying
+    // a v_readlane (a VALU instruction) at every use.  Scalar loads hit the
+    // constant cache.  This `a` shadows the parameter inside the loop.
+    typedef __attribute__((address_space(4))) const TraceArgs cst_args;
+    const cst_args *apc = (const cst_args *)((__attribute__((address_space(4))) const char *)
+                                                 __builtin_amdgcn_kernarg_segment_ptr() + kTraceArgsOffset);
+    asm volatile("" : "+s"(apc));
+    const TraceArgs a = *apc;
+#endif
     if (next >= end && !exhausted) {  // wave-uniform: the next chunk (full exec here)
       // One counter, grabbed when needed.  Measured against alternatives
       // (profiles/r02_variants_chunk_*.log): 8 counters on separate lines
@@ -1272,7 +1292,11 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       // contribution.  The per-lane sweep ran on the ~1/3 of lanes whose path
       // just ended while the rest idled.
       const int Kf = (finished && k > 0) ? k : 0;
+#ifdef IPT_ABL_NOWSWEEP  // timing-only ablation build: no backward sweep (no gradients)
+      if (0) {
+#else
       if (__ballot(Kf > 0)) {
+#endif
         const int lane = tid & 63;
         int inc = Kf;  // inclusive scan of the task counts over the wave
         for (int dd = 1; dd < 64; dd <<= 1) {
@@ -1370,7 +1394,11 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             }
             const int sl = a.grad_map ? a.grad_map[tk] : tk;
             const double v[3] = {(double)(ax * gk.x), (double)(ay * gk.y), (double)(az * gk.z)};
+#ifdef IPT_ABL_NOATOMIC  // timing-only ablation build: contributions computed, not accumulated
+            if (v[0] == 12345.0) lds_acc[0] = v[1] + v[2];
+#else
             bins_add(sl >= 0, grad, sl >= 0 ? (size_t)sl * 3 : (size_t)tk * 3, 3, v);
+#endif
           }
         }
       }
