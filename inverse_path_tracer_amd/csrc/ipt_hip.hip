@@ -72,10 +72,10 @@ constexpr int kBlock = 256;
 // shadow ray failed), coeff; with a Phong lobe also specd and speci.
 // With IPT_ADJ_STORE_M the record also keeps the vertex's prefix throughput
 // M (the forward's own value), so the sweep is O(K) instead of recomputing
-// every prefix product (O(K^2)); costs 3 words per vertex of LDS, which drops
-// the adjoint from 6 to 5 blocks per CU at max_bounces = 4.  Measured
-// (profiles/r01_variants_adj_store_m.log): -3.4% on C2 (18 triangles), +4.4%
-// on C3 (30 triangles) -- off by default.
+// every prefix product (O(K^2)); costs 3 words per vertex of LDS.  Measured
+// with the wave sweep reading it, at 5 waves/SIMD: C2 adjoint 2.41 -> 2.66 ms
+// (2.59 without the camera-ray ring, which keeps 5 blocks per CU), scenes/0
+// 2.95 -> 3.20 (profiles/r02_variants_adj_sweep.log) -- off by default.
 #ifndef IPT_ADJ_STORE_M
 #define IPT_ADJ_STORE_M 0
 #endif
@@ -1372,13 +1372,19 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
               S = mk((LeL.x + dj.x * lk.x) + (tjv.x * cj) * S.x, (LeL.y + dj.y * lk.y) + (tjv.y * cj) * S.y,
                      (LeL.z + dj.z * lk.z) + (tjv.z * cj) * S.z);
             }
-            // prefix throughput M_kk
+            // prefix throughput M_kk: recorded by the forward (IPT_ADJ_STORE_M) or
+            // recomputed with exactly its operations
             V3 Mk = mk(1.f, 1.f, 1.f);
-            for (int j = 0; j < kk; ++j) {
-              const float *r = col + (size_t)j * kBlock;
-              const float cj = r[2 * fs];
-              const V3 tjv = tdiff((int)(__float_as_uint(r[0]) & 0xffffu), r);
-              Mk = mk((Mk.x * tjv.x) * cj, (Mk.y * tjv.y) * cj, (Mk.z * tjv.z) * cj);
+            if (IPT_ADJ_STORE_M) {
+              const float *r = col + (size_t)kk * kBlock;
+              Mk = mk(r[kRecM * fs], r[(kRecM + 1) * fs], r[(kRecM + 2) * fs]);
+            } else {
+              for (int j = 0; j < kk; ++j) {
+                const float *r = col + (size_t)j * kBlock;
+                const float cj = r[2 * fs];
+                const V3 tjv = tdiff((int)(__float_as_uint(r[0]) & 0xffffu), r);
+                Mk = mk((Mk.x * tjv.x) * cj, (Mk.y * tjv.y) * cj, (Mk.z * tjv.z) * cj);
+              }
             }
             const float *r = col + (size_t)kk * kBlock;
             const uint32_t f0 = __float_as_uint(r[0]);
