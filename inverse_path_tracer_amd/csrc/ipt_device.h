@@ -734,13 +734,19 @@ __device__ __forceinline__ SlabRay slab_ray(V3 p, V3 d) {
 #ifndef IPT_SHADOW_CULL
 #define IPT_SHADOW_CULL 1
 #endif
-__device__ __forceinline__ int shadow_hit_pairs_small(const TriIsect *__restrict__ isect,
-                                                      const TriPair *__restrict__ pairs,
+__device__ __forceinline__ int shadow_hit_pairs_small(const lds_f32 *isect_lds, const TriPair *__restrict__ pairs,
                                                       const PairBox2 *__restrict__ boxes, const f2 *e3, int nT, V3 p,
                                                       V3 d, int target, float &best_t) {
   float bt = __builtin_inff();
   int bi = -1;
-  hit_test(isect[target], target, p, d, bt, bi);
+  {  // the target's record from the LDS copy of the TriIsect array
+    TriIsect T;
+    float *tf = reinterpret_cast<float *>(&T);
+    const lds_f32 *q = isect_lds + 20 * target;
+#pragma unroll
+    for (int k = 0; k < 20; ++k) tf[k] = q[k];
+    hit_test(T, target, p, d, bt, bi);
+  }
   bool live = bi >= 0;
   int nP = (nT + 1) >> 1;
   asm volatile("" : "+s"(nP));

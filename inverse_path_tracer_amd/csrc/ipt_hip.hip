@@ -558,7 +558,15 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     for (int i = tid; i < kE3Floats * nP; i += nthr) lds_e3[i] = small_table_entry(pairs, i);
     e3 = reinterpret_cast<const f2 *>(lds_e3);
   }
-  float *lds_rec = lds_e3 + (a.small_pairs ? kE3Floats * nP : 0);
+  // small scenes: a copy of the TriIsect records (16-B aligned), read by the
+  // culled shadow cast's per-lane target test from LDS instead of L2
+  float *lds_is = lds_e3 + (a.small_pairs ? kE3Floats * nP : 0);
+  lds_is += (4 - (int)((lds_is - reinterpret_cast<float *>(lds)) & 3)) & 3;
+  if (a.small_pairs) {
+    const float *g = reinterpret_cast<const float *>(isect);
+    for (int i = tid; i < 20 * nT; i += nthr) lds_is[i] = g[i];
+  }
+  float *lds_rec = a.small_pairs ? lds_is + 20 * nT : lds_e3;
   // Camera-ray ring (RING instances): per wave kRingFields x 64 words after the
   // ADJ records, then the camera origin (3 floats per wave).
   const bool RING = ring_on<MODE, BVH>() && a.use_ring;
@@ -976,7 +984,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         coop_cast<true>(cv, qn, p, sd, ts, hs);
       } else if (!SERVE && shadow) {
         if (!BVH && IPT_SHADOW_CULL && e3)
-          hs = shadow_hit_pairs_small(isect, pairs, a.pboxes, e3, nT, p, sd, et, ts);
+          hs = shadow_hit_pairs_small((const lds_f32 *)lds_is, pairs, a.pboxes, e3, nT, p, sd, et, ts);
         else
           hs = cast<BVH>(isect, pairs, e3, nT, bv, p, sd, ts, et);
       }
@@ -1806,7 +1814,8 @@ static size_t bvh_lds(const GpuScene *s, TraceArgs &a, size_t base, bool server)
 
 static size_t table_bytes(const TraceArgs &a) {
   return (a.kd_tables ? (size_t)6 * a.nT * sizeof(float) : 0) +
-         (a.small_pairs ? (size_t)kE3Floats * ((a.nT + 1) / 2) * sizeof(float) : 0);
+         (a.small_pairs ? (size_t)kE3Floats * ((a.nT + 1) / 2) * sizeof(float) + 12 + (size_t)a.nT * sizeof(TriIsect)
+                        : 0);
 }
 
 // Per-launch scratch (the fused render's sample buffer, kd/pi of large
