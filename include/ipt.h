@@ -132,7 +132,8 @@ int ipt_scene_export_wide(void *scene, float *wide, uint32_t *qwide);
  * own cast: idx = triangle index or -1, t = its distance.  targets
  * (nullable, n ints): >= 0 marks a next-event shadow ray towards that
  * emitter triangle, for which only "idx == target" and then t are defined
- * (the BVH stops once the target is known to be occluded). */
+ * (the BVH stops once the target is known to be occluded; small scenes use
+ * the megakernel's culled shadow cast, which reports -1 when occluded). */
 int ipt_closest_hit_host(void *scene, int64_t n, const float *origins, const float *dirs, const int32_t *targets,
                          float *t, int32_t *idx);
 int ipt_closest_hit_dev(void *scene, int64_t n, const float *origins_dev, const float *dirs_dev,

@@ -1247,14 +1247,17 @@ __device__ __forceinline__ V3 shading_normal(const TriGeom &g, V3 q) {
 }
 
 // Camera ray (path_trace.cu:155-165) + Ray::transform (scene_basics.h:307-319)
-__device__ __forceinline__ void camera_ray(const float *cam, Rng &st, int r, int c, int W, int H, V3 &p,
-                                           V3 &d) {
+// rcW / rcH: 1/W and 1/H when W and H are powers of two (then x * rcW == x / W
+// exactly: a power-of-two scale of a normal float), else 0 (divide).
+__device__ __forceinline__ void camera_ray(const float *cam, Rng &st, int r, int c, int W, int H, float rcW,
+                                           float rcH, V3 &p, V3 &d) {
   const float u0 = uniform(st), u1 = uniform(st);
   // (2(c+u0)) / W: numerator in [2^-32, 2W], W >= 1 -- in div_inrange's range.
   // d0 = (x, y, 1): x and y are 0 or multiples of 2^-24 (Sterbenz), n2 in
   // [1, 3] -- in unit_in_range's range.
-  const float x = div_inrange(2.f * ((float)c + u0), (float)W) - 1.f;
-  const float y = 1.f - div_inrange(2.f * ((float)r + u1), (float)H);
+  const float nx = 2.f * ((float)c + u0), ny = 2.f * ((float)r + u1);
+  const float x = (rcW != 0.f ? nx * rcW : div_inrange(nx, (float)W)) - 1.f;
+  const float y = 1.f - (rcH != 0.f ? ny * rcH : div_inrange(ny, (float)H));
   const V3 d0 = unit_in_range(mk(x, y, 1.f));
   float pr[3], dr[3];
 #pragma unroll

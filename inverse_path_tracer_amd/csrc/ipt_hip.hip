@@ -178,6 +178,7 @@ struct TraceArgs {
   // 1/spp when spp is a power of two (then x * rc_spp == x / spp for every
   // float x: both are the correctly rounded x * 2^-k), else 0
   float rc_spp;
+  float rc_W, rc_H;  // 1/W, 1/H for power-of-two sizes, else 0 (camera_ray divides)
   int use_ring;  // RING instances: camera rays from the LDS ring (host decides: only if it costs no residency)
   int rec_cap;   // ADJ: vertex records per lane (max_bounces + 1); ADJU: ring slots
   // scene batch (C5): blocks b, b + nscenes, ... (bps of them) trace material
@@ -270,7 +271,7 @@ __device__ __forceinline__ void item_ray(const TraceArgs &a, uint64_t seed, uint
     g = ((uint64_t)r * (uint64_t)a.W + (uint64_t)c) * (uint64_t)a.spp + sj;
   }
   rng_init(st, seed + g);
-  camera_ray(a.cam, st, r, c, a.W, a.H, p, d);
+  camera_ray(a.cam, st, r, c, a.W, a.H, a.rc_W, a.rc_H, p, d);
 }
 
 // ---------------------------------------------------------------------------
@@ -1777,6 +1778,8 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.out_stride = a.n_samples * 3;
   a.adj_stride = (uint64_t)p.width * p.height * 3;
   a.rc_spp = (p.spp > 0 && p.spp <= (1 << 24) && (p.spp & (p.spp - 1)) == 0) ? 1.0f / (float)p.spp : 0.f;
+  a.rc_W = (p.width > 0 && (p.width & (p.width - 1)) == 0) ? 1.0f / (float)p.width : 0.f;
+  a.rc_H = (p.height > 0 && (p.height & (p.height - 1)) == 0) ? 1.0f / (float)p.height : 0.f;
   return a;
 }
 
@@ -2121,9 +2124,10 @@ int gpu_selftest_math(uint64_t n, uint64_t seed, uint64_t *counts_host) {
 // The cast() of the megakernel on caller-supplied rays: one ray per thread,
 // the same LDS staging (small-scene plane offsets, BVH nodes + stack).
 // targets[i] >= 0 makes ray i a shadow ray towards that emitter triangle
-// (the BVH then answers only "is the closest hit the target, and at which
-// t"; the brute-force loop always returns the full closest hit).  Used by
-// the exactness tests of the BVH against the brute-force loop.
+// (the BVH and the small scenes' culled shadow cast then answer only "is the
+// closest hit the target, and at which t"; without targets the brute-force
+// loop returns the full closest hit).  Used by the exactness tests of the
+// BVH and of the shadow cull against the brute-force loop.
 template <bool BVH>
 __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__restrict__ isect,
                                                              const TriPair *__restrict__ pairs,
@@ -2142,6 +2146,13 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
   if (small) {
     for (int i = tid; i < kE3Floats * nP; i += kBlock) lds_e3[i] = small_table_entry(pairs, i);
     e3 = reinterpret_cast<const f2 *>(lds_e3);
+  }
+  // the culled shadow cast's LDS copy of the TriIsect records (!BVH, small)
+  float *lds_is = lds_e3 + kE3Floats * nP;
+  lds_is += (4 - (int)((lds_is - lds_e3) & 3)) & 3;
+  if (!BVH && small) {
+    const float *g = reinterpret_cast<const float *>(isect);
+    for (int i = tid; i < 20 * nT; i += kBlock) lds_is[i] = g[i];
   }
   BvhView bv;
   bv.nodes = bnodes;
@@ -2212,7 +2223,10 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
     coop_cast<false>(cv, qn && target < 0, p, d, t, h);
     coop_cast<true>(cv, qn && target >= 0, p, d, t, h);
   } else if (valid) {
-    h = cast<BVH>(isect, pairs, e3, nT, bv, p, d, t, target);
+    if (!BVH && IPT_SHADOW_CULL && small && target >= 0)  // the megakernel's shadow cast of small scenes
+      h = shadow_hit_pairs_small((const lds_f32 *)lds_is, pairs, a.pboxes, e3, nT, p, d, target, t);
+    else
+      h = cast<BVH>(isect, pairs, e3, nT, bv, p, d, t, target);
   }
   if (valid) {
     t_out[i] = t;
@@ -2250,7 +2264,8 @@ int gpu_closest_hit(GpuScene *s, int64_t n, const float *org_dev, const float *d
     hipLaunchKernelGGL(closest_hit_kernel<true>, dim3(blocks), dim3(kBlock), lds, (hipStream_t)stream, s->isect,
                        s->pairs, s->bnodes, s->bpairs, a, small, n, org_dev, dir_dev, targets_dev, t_dev, idx_dev);
   } else {
-    hipLaunchKernelGGL(closest_hit_kernel<false>, dim3(blocks), dim3(kBlock), base, (hipStream_t)stream, s->isect,
+    const size_t lds = base + (small ? 12 + (size_t)s->host.nT * sizeof(TriIsect) : 0);
+    hipLaunchKernelGGL(closest_hit_kernel<false>, dim3(blocks), dim3(kBlock), lds, (hipStream_t)stream, s->isect,
                        s->pairs, s->bnodes, s->bpairs, a, small, n, org_dev, dir_dev, targets_dev, t_dev, idx_dev);
   }
   HIP_TRY(hipGetLastError());

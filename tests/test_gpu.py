@@ -517,3 +517,46 @@ def test_bvh_renders_equal_brute_force_and_oracle(oracle):
     np.testing.assert_allclose(P.adjoint(adj, W, H, spp, mb, seed), Q.adjoint(W, H, spp, mb, seed, adj),
                                rtol=1e-9, atol=1e-12)
     P.set_accel(N.ACCEL_AUTO)
+
+
+@pytest.mark.parametrize("which", ["cornell", "scene0"])
+def test_culled_shadow_query_equals_brute_force(which):
+    """Small scenes: the megakernel's culled shadow cast (target first, pairs
+    skipped by acceptance box over [1e-2, t_target]) answers "closest hit is
+    the target, at t" exactly as the full brute-force loop, for shadow rays
+    from points on every triangle (grazing ones included) and from random
+    points inside the scene box, towards points on the emitters (edges and
+    corners included)."""
+    P = product_scene(CORNELL if which == "cornell" else SCENE0)
+    tris = P.triangles()
+    emit = np.nonzero(tris[:, 56] >= 0)[0]
+    assert len(emit) >= 1
+    rng = np.random.RandomState(21)
+    n = 400000
+    v = tris[:, 0:9].reshape(-1, 3, 3)
+
+    def on_tri(idx, a, b):
+        flip = a + b > 1
+        a, b = np.where(flip, 1 - a, a), np.where(flip, 1 - b, b)
+        return v[idx, 0] + a[:, None] * (v[idx, 1] - v[idx, 0]) + b[:, None] * (v[idx, 2] - v[idx, 0])
+
+    src = rng.randint(0, P.nT, n)
+    O = on_tri(src, *rng.uniform(0, 1, (2, n)))
+    box = v.reshape(-1, 3)
+    inside = rng.uniform(0, 1, n) < 0.2
+    O[inside] = rng.uniform(box.min(0), box.max(0), (int(inside.sum()), 3))
+    tg = emit[rng.randint(0, len(emit), n)]
+    ab = rng.uniform(0, 1, (2, n))
+    edge = rng.uniform(0, 1, n) < 0.3  # targets on or next to the emitter's edges and corners
+    ab[:, edge] = np.round(ab[:, edge] * 4) / 4 + rng.normal(0, 1e-6, (2, int(edge.sum())))
+    pt = on_tri(tg, np.clip(ab[0], 0, 1), np.clip(ab[1], 0, 1))
+    D = pt - O
+    D /= np.linalg.norm(D, axis=1, keepdims=True)
+    O, D = O.astype(np.float32), D.astype(np.float32)
+    tc, ic = P.closest_hit(O, D, targets=tg)
+    tf, i_f = P.closest_hit(O, D)
+    vis_c, vis_f = ic == tg, i_f == tg
+    assert np.array_equal(vis_c, vis_f)
+    assert 0.05 < vis_f.mean() < 0.98
+    assert np.array_equal(bits(tc[vis_c]), bits(tf[vis_f]))
+    P.close()
