@@ -513,6 +513,7 @@ bool build_bvh(HostScene *S) {
   S->bvh_pairs.clear();
   S->bvh_big_pairs.clear();
   S->bvh_big_idx.clear();
+  S->bvh_big_boxes.clear();
   S->bvh_depth = 0;
   const double r_all = scene_coord_bound(*S);
   Builder B;
@@ -560,11 +561,36 @@ bool build_bvh(HostScene *S) {
       S->bvh_big_idx[k] = big[k];
     }
     if (np > 0) pack_pairs(recs.data(), 2 * np, S->bvh_big_pairs.data());
+    // acceptance boxes of the big pairs, two pairs per record (as pair_boxes)
+    const float inf = std::numeric_limits<float>::infinity();
+    S->bvh_big_boxes.assign((size_t)(np + 1) / 2, PairBox2());
+    for (int j = 0; j < np; ++j) {
+      float lo[3] = {inf, inf, inf}, hi[3] = {-inf, -inf, -inf};
+      bool any = false;
+      for (int h = 0; h < 2; ++h) {
+        const size_t k = (size_t)(2 * j + h);
+        if (k >= big.size()) continue;
+        float l[3], u[3];
+        if (acceptance_box(S->isect[(size_t)big[k]], S->geom[(size_t)big[k]], r_all, l, u) != 0) continue;
+        any = true;
+        for (int a = 0; a < 3; ++a) {
+          lo[a] = std::min(lo[a], l[a]);
+          hi[a] = std::max(hi[a], u[a]);
+        }
+      }
+      for (int a = 0; a < 3; ++a) {
+        S->bvh_big_boxes[(size_t)j / 2].f[2 * a][j & 1] = any ? lo[a] : inf;
+        S->bvh_big_boxes[(size_t)j / 2].f[2 * a + 1][j & 1] = any ? hi[a] : inf;
+      }
+    }
+    if (np & 1)
+      for (int k = 0; k < 6; ++k) S->bvh_big_boxes.back().f[k][1] = inf;
   }
   if (B.prims.size() < 2) {
     S->bvh_status = "fewer than two hittable triangles outside the brute-force set";
     S->bvh_big_pairs.clear();
     S->bvh_big_idx.clear();
+    S->bvh_big_boxes.clear();
     return false;
   }
   Box root_box;
@@ -640,6 +666,7 @@ bool build_bvh(HostScene *S) {
     S->bvh_pairs.clear();
     S->bvh_big_pairs.clear();
     S->bvh_big_idx.clear();
+    S->bvh_big_boxes.clear();
     return false;
   }
   S->bvh_status = "ok";

@@ -595,6 +595,7 @@ struct BvhView {
   const int32_t *big_idx;   // original indices, 2 per pair
   const f2 *big_e3;         // LDS: the pairs' edge-plane offsets
   int nbig;                 // pairs (<= kSmallPairs)
+  const PairBox2 *big_boxes;  // the pairs' acceptance boxes (culled shadow pre-pass)
 };
 constexpr int kStackStride = 256;  // = the megakernel's block size
 constexpr int kBvhDone = (int)0x80000000;
@@ -734,6 +735,67 @@ __device__ __forceinline__ SlabRay slab_ray(V3 p, V3 d) {
 #ifndef IPT_SHADOW_CULL
 #define IPT_SHADOW_CULL 1
 #endif
+// Bit j: the ray enters pair j's acceptance box within [kEpsUp, bt] (the
+// pairs' boxes two per PairBox2 record; scalar loads).
+__device__ __forceinline__ uint32_t pair_box_bits(const PairBox2 *boxes, int nP, V3 p, V3 d, float bt) {
+  uint32_t need = 0;
+  const SlabRay r = slab_ray(p, d);
+#pragma unroll
+  for (int J = 0; J < kSmallPairs / 2; ++J) {
+    if (2 * J < nP) {  // wave-uniform
+      const cst_f32 *B = (const cst_f32 *)(boxes + J);
+      const f2 tx0 = fma2(f2{B[0], B[1]}, r.ix, r.ox), tx1 = fma2(f2{B[2], B[3]}, r.ix, r.ox);
+      const f2 ty0 = fma2(f2{B[4], B[5]}, r.iy, r.oy), ty1 = fma2(f2{B[6], B[7]}, r.iy, r.oy);
+      const f2 tz0 = fma2(f2{B[8], B[9]}, r.iz, r.oz), tz1 = fma2(f2{B[10], B[11]}, r.iz, r.oz);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float en =
+            fmaxf(fmaxf(fminf(tx0[h], tx1[h]), fminf(ty0[h], ty1[h])), fmaxf(fminf(tz0[h], tz1[h]), kEpsUp));
+        const float ex = fminf(fminf(fmaxf(tx0[h], tx1[h]), fmaxf(ty0[h], ty1[h])), fminf(fmaxf(tz0[h], tz1[h]), bt));
+        need |= (en <= ex ? 1u : 0u) << (2 * J + h);
+      }
+    }
+  }
+  return need;
+}
+
+// The occlusion part of a culled shadow cast over nP pairs (pair_at(j):
+// the TriPair, idx_at(k): original triangle index k of the pass, e3l: the
+// pairs' plane offsets in LDS).  A pair is tested only when some live lane's
+// box bit is set; only "is the target still the lexicographic minimum"
+// matters, so bt stays t_e: pair triangle i occludes iff it is accepted with
+// t < t_e, or t == t_e and i < target, i.e. t < bound_i with bound_i =
+// nextup(t_e) for i < target (t_e >= kEpsUp > 0 is finite: +1 on the bits is
+// nextup).  Returns the lane's "still visible".
+typedef __attribute__((address_space(3))) const f2 lds_f2c;
+template <class PairAt, class IdxAt>
+__device__ __forceinline__ bool occlusion_pass(PairAt pair_at, IdxAt idx_at, lds_f2c *e3l, int nP, uint32_t need, V3 p,
+                                               V3 d, int target, float te, bool live) {
+  const float teu = __uint_as_float(__float_as_uint(te) + 1u);
+#pragma unroll
+  for (int j = 0; j < kSmallPairs; ++j) {
+    if (j < nP) {  // wave-uniform
+      if (__builtin_amdgcn_ballot_w64(live && ((need >> j) & 1u))) {
+#ifdef IPT_BVH_STATS
+        if (__lane_id() == __ffsll((unsigned long long)__builtin_amdgcn_ballot_w64(true)) - 1)
+          atomicAdd(&g_bvh_stats[15], 1ull);                // wave-level pair tests
+#endif
+        if (live) {
+#ifdef IPT_BVH_STATS
+          atomicAdd(&g_bvh_stats[16], 1ull);                // lane pair tests
+#endif
+          const TriPair T = pair_at(j);
+          const bool occ = pair_occludes(T, pair_origin(T, p), idx_at(2 * j) < target ? teu : te,
+                                         idx_at(2 * j + 1) < target ? teu : te, p, d, e3l[3 * j], e3l[3 * j + 1],
+                                         e3l[3 * j + 2]);
+          live = live && !occ;
+        }
+      }
+    }
+  }
+  return live;
+}
+
 __device__ __forceinline__ int shadow_hit_pairs_small(const lds_f32 *isect_lds, const TriPair *__restrict__ pairs,
                                                       const PairBox2 *__restrict__ boxes, const f2 *e3, int nT, V3 p,
                                                       V3 d, int target, float &best_t) {
@@ -750,8 +812,7 @@ __device__ __forceinline__ int shadow_hit_pairs_small(const lds_f32 *isect_lds, 
   bool live = bi >= 0;
   int nP = (nT + 1) >> 1;
   asm volatile("" : "+s"(nP));
-  typedef __attribute__((address_space(3))) const f2 lds_f2;
-  lds_f2 *e3l = (lds_f2 *)e3;
+  lds_f2c *e3l = (lds_f2c *)e3;
   if (IPT_PIN_E3) asm volatile("" : "+v"(e3l));
 #ifdef IPT_BVH_STATS
   atomicAdd(&g_bvh_stats[12], 1ull);                      // shadow lanes
@@ -764,60 +825,11 @@ __device__ __forceinline__ int shadow_hit_pairs_small(const lds_f32 *isect_lds, 
   // box loads out of the megakernel loop into SGPRs, which then spill
   asm volatile("" : "+s"(boxes));
   if (__builtin_amdgcn_ballot_w64(live)) {
-    // (a) this lane's candidate pairs: bit j = its ray enters pair j's box
-    // within [kEpsUp, bt] (computed first, so that the slab registers are
-    // dead before the pair tests)
-    uint32_t need = 0;
-    {
-      const SlabRay r = slab_ray(p, d);
-#pragma unroll
-      for (int J = 0; J < kSmallPairs / 2; ++J) {
-        if (2 * J < nP) {  // wave-uniform
-          const cst_f32 *B = (const cst_f32 *)(boxes + J);  // scalar loads
-          const f2 tx0 = fma2(f2{B[0], B[1]}, r.ix, r.ox), tx1 = fma2(f2{B[2], B[3]}, r.ix, r.ox);
-          const f2 ty0 = fma2(f2{B[4], B[5]}, r.iy, r.oy), ty1 = fma2(f2{B[6], B[7]}, r.iy, r.oy);
-          const f2 tz0 = fma2(f2{B[8], B[9]}, r.iz, r.oz), tz1 = fma2(f2{B[10], B[11]}, r.iz, r.oz);
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const float en = fmaxf(fmaxf(fminf(tx0[h], tx1[h]), fminf(ty0[h], ty1[h])),
-                                   fmaxf(fminf(tz0[h], tz1[h]), kEpsUp));
-            const float ex = fminf(fminf(fmaxf(tx0[h], tx1[h]), fmaxf(ty0[h], ty1[h])),
-                                   fminf(fmaxf(tz0[h], tz1[h]), bt));
-            need |= (en <= ex ? 1u : 0u) << (2 * J + h);
-          }
-        }
-      }
-    }
-    // (b) the pairs some live lane needs, in index order.  Only "is the
-    // target still the lexicographic minimum" matters, so bt stays t_e: pair
-    // triangle i occludes iff it is accepted with t < t_e, or t == t_e and
-    // i < target, i.e. t < bound_i with bound_i = nextup(t_e) for i < target
-    // (t_e >= kEpsUp > 0 is finite: +1 on the bits is nextup).
-    const float te = bt, teu = __uint_as_float(__float_as_uint(bt) + 1u);
-#pragma unroll
-    for (int j = 0; j < kSmallPairs; ++j) {
-      if (j < nP) {  // wave-uniform
-        if (__builtin_amdgcn_ballot_w64(live && ((need >> j) & 1u))) {
-#ifdef IPT_BVH_STATS
-          if (__lane_id() == __ffsll((unsigned long long)__builtin_amdgcn_ballot_w64(true)) - 1)
-            atomicAdd(&g_bvh_stats[15], 1ull);                // wave-level pair tests
-#endif
-          if (live) {
-#ifdef IPT_BVH_STATS
-            atomicAdd(&g_bvh_stats[16], 1ull);                // lane pair tests
-#endif
-            const TriPair T = pairs[j];
-            const bool occ = pair_occludes(T, pair_origin(T, p), 2 * j < target ? teu : te,
-                                           2 * j + 1 < target ? teu : te, p, d, e3l[3 * j], e3l[3 * j + 1],
-                                           e3l[3 * j + 2]);
-            if (occ) {
-              live = false;
-              bi = -1;  // not the target (the caller only compares with it)
-            }
-          }
-        }
-      }
-    }
+    // box bits first, so that the slab registers are dead before the pair tests
+    const uint32_t need = pair_box_bits(boxes, nP, p, d, bt);
+    live = occlusion_pass([&](int j) { return pairs[j]; }, [&](int k) { return k; }, e3l, nP, need, p, d, target, bt,
+                          live);
+    if (!live && bi >= 0) bi = -1;  // occluded: not the target (the caller only compares with it)
   }
   best_t = bt;
   return bi;
@@ -857,7 +869,8 @@ __device__ __forceinline__ bool bvh_prepass(const BvhView &B, V3 p, V3 d, float 
 #endif
 #ifdef IPT_BVH_STATS
   atomicAdd(&g_bvh_stats[7], 1ull);
-  atomicAdd(&g_bvh_stats[8], 2ull * (unsigned long long)B.nbig);
+  if (!(SHADOW && IPT_SHADOW_CULL)) atomicAdd(&g_bvh_stats[8], 2ull * (unsigned long long)B.nbig);
+  if (SHADOW && IPT_SHADOW_CULL) atomicAdd(&g_bvh_stats[17], (unsigned long long)B.nbig);  // lane box tests
   if (SHADOW) atomicAdd(&g_bvh_stats[9], 1ull);
 #endif
   if (SHADOW) {
@@ -869,7 +882,28 @@ __device__ __forceinline__ bool bvh_prepass(const BvhView &B, V3 p, V3 d, float 
       return false;
     }
   }
-  if (B.nbig > 0) {
+  if (SHADOW && IPT_SHADOW_CULL && B.nbig > 0) {
+    // the large triangles as in the small scenes' culled shadow cast: only
+    // the pairs whose acceptance box some lane's ray enters within
+    // [kEpsUp, t_target], reduced to "does it occlude the target"
+    int nP = B.nbig;
+    asm volatile("" : "+s"(nP));
+    lds_f2c *e3l = (lds_f2c *)B.big_e3;
+    if (IPT_PIN_E3) asm volatile("" : "+v"(e3l));
+    const cst_i32 *bidx = (const cst_i32 *)B.big_idx;
+    const PairBox2 *boxes = B.big_boxes;
+    asm volatile("" : "+s"(boxes));
+    const uint32_t need = pair_box_bits(boxes, nP, p, d, bt);
+    const bool vis = occlusion_pass([&](int j) { return load_pair_cst(B.big + j); }, [&](int k) { return bidx[k]; },
+                                    e3l, nP, need, p, d, target, bt, true);
+    if (!vis) {  // occluded by a large triangle: decided
+      bi = -1;
+#ifdef IPT_BVH_STATS
+      atomicAdd(&g_bvh_stats[10], 1ull);
+#endif
+      return false;
+    }
+  } else if (B.nbig > 0) {
     bvh_big_pass<SHADOW>(B, p, d, bt, bi);
     if (SHADOW && bi != target) {  // occluded by a large triangle: decided
 #ifdef IPT_BVH_STATS

@@ -167,6 +167,7 @@ struct TraceArgs {
   float root_box[6];
   const TriPair *bvh_big;
   const int32_t *bvh_big_idx;
+  const PairBox2 *bvh_big_boxes;
   // ADJ gradient bins: grad_slots triangles accumulate in LDS fp64 (all of
   // them when they fit, else the largest -- the most-hit -- ones, mapped by
   // grad_map[tri] -> slot or -1, slot_tri[slot] -> tri); the rest go to
@@ -586,6 +587,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   bv.big_idx = nullptr;
   bv.big_e3 = nullptr;
   bv.nbig = 0;
+  bv.big_boxes = nullptr;
   CoopView cv;
   cv.wn = nullptr;
   cv.wn_lds = false;
@@ -619,6 +621,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     }
     bv.big = a.bvh_big;
     bv.big_idx = a.bvh_big_idx;
+    bv.big_boxes = a.bvh_big_boxes;
     bv.big_e3 = reinterpret_cast<const f2 *>(be3);
     bv.nbig = a.bvh_nbig;
     float *after = be3 + 6 * a.bvh_nbig;
@@ -1531,6 +1534,7 @@ struct GpuScene {
   BvhPair *bpairs = nullptr;
   TriPair *big_pairs = nullptr;
   int32_t *big_idx = nullptr;
+  PairBox2 *big_boxes = nullptr;
   float4 *wide = nullptr;  // WideNode or QWideNode records (IPT_BVH_QNODES)
   TriIsect *wtris = nullptr;
   PairBox2 *pboxes = nullptr;  // pair acceptance boxes (small scenes' culled shadow casts)
@@ -1590,6 +1594,7 @@ GpuScene *gpu_upload(const HostScene &host, std::string *err) {
       upload(&s->kd, host.kd) || upload(&s->emit_tri, host.emit_tri) || upload(&s->emit_cdf, host.emit_cdf) ||
       upload(&s->emit_pmf, host.emit_pmf) || upload(&s->bnodes, host.bvh_nodes) || upload(&s->bpairs, host.bvh_pairs) ||
       upload(&s->big_pairs, host.bvh_big_pairs) || upload(&s->big_idx, host.bvh_big_idx) ||
+      upload(&s->big_boxes, host.bvh_big_boxes) ||
       (IPT_BVH_QNODES ? upload_as_f4(&s->wide, host.bvh_qwide) : upload_as_f4(&s->wide, host.bvh_wide)) ||
       upload(&s->wtris, host.bvh_wtris) || upload(&s->pboxes, pair_boxes(host))) {
     *err = gpu_last_error();
@@ -1651,6 +1656,7 @@ void gpu_free(GpuScene *s) {
   (void)hipFree(s->bpairs);
   (void)hipFree(s->big_pairs);
   (void)hipFree(s->big_idx);
+  (void)hipFree(s->big_boxes);
   (void)hipFree(s->wide);
   (void)hipFree(s->wtris);
   (void)hipFree(s->pboxes);
@@ -1758,6 +1764,7 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.bvh_nbig = 0;
   a.bvh_big = nullptr;
   a.bvh_big_idx = nullptr;
+  a.bvh_big_boxes = nullptr;
   a.bvh_wide = nullptr;
   a.bvh_wtris = nullptr;
   a.bvh_wide_lds = 0;
@@ -1807,6 +1814,7 @@ static size_t bvh_lds(const GpuScene *s, TraceArgs &a, size_t base, bool server)
   a.bvh_nbig = (int)s->host.bvh_big_pairs.size();
   a.bvh_big = s->big_pairs;
   a.bvh_big_idx = s->big_idx;
+  a.bvh_big_boxes = s->big_boxes;
   const size_t head = bvh_lds_offset(base) + (size_t)a.bvh_lds_nodes * sizeof(BvhNode) +
                       (size_t)a.bvh_wide_lds * kWideF4 * sizeof(float4) + (size_t)a.bvh_nbig * 6 * sizeof(float);
   if (kCoop) return head + (size_t)(kBlock / 64) * 8 * a.coop_stride * sizeof(uint32_t);
@@ -2164,6 +2172,7 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
   bv.big_idx = nullptr;
   bv.big_e3 = nullptr;
   bv.nbig = 0;
+  bv.big_boxes = nullptr;
   CoopView cv;
   cv.wn = a.bvh_wide;
   cv.wn_lds = false;
@@ -2192,6 +2201,7 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
     }
     bv.big = a.bvh_big;
     bv.big_idx = a.bvh_big_idx;
+    bv.big_boxes = a.bvh_big_boxes;
     bv.big_e3 = reinterpret_cast<const f2 *>(be3);
     bv.nbig = a.bvh_nbig;
     uint32_t *after = reinterpret_cast<uint32_t *>(be3 + 6 * a.bvh_nbig);

@@ -36,6 +36,7 @@ struct HostScene {
   // pairs in ascending original index, padded with zero triangles
   std::vector<TriPair> bvh_big_pairs;
   std::vector<int32_t> bvh_big_idx;  // 2 per pair; 0x7fffffff = padding
+  std::vector<PairBox2> bvh_big_boxes;  // their acceptance boxes (culled shadow pre-pass)
   // the same tree collapsed to 8-wide nodes for the cooperative traversal
   std::vector<WideNode> bvh_wide;   // breadth-first, root 0
   std::vector<QWideNode> bvh_qwide; // the same nodes quantised (scene_layout.h)
