@@ -36,6 +36,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 
@@ -50,7 +51,7 @@ constexpr double kCostNode = 1.0, kCostPair = 1.0;
 // box's surface area (almost every ray reaches them: room walls) are tested
 // by the unrolled brute-force pair loop ahead of the traversal, up to 2 *
 // kBigPairs of them, instead of sitting in leaves that every ray visits.
-constexpr double kBigFrac = 1.0 / 32;
+constexpr double kBigFrac = 1.0 / 64;  // 1/32 left the cube of the north-star scene in the tree: fwd 5.27 -> 4.50 ms at 1/64 (profiles/r02_bigfrac_ab.log)
 constexpr int kBigPairs = 16;  // = ipt_device.h kSmallPairs
 
 struct Box {
@@ -533,7 +534,9 @@ bool build_bvh(HostScene *S) {
   {
     Box all;
     for (const Prim &p : B.prims) all.grow(p.box);
-    const double lim = kBigFrac * all.area();
+    // IPT_BVH_BIGFRAC (A/B timing only) overrides the threshold
+    const char *bf = std::getenv("IPT_BVH_BIGFRAC");
+    const double lim = (bf ? std::atof(bf) : kBigFrac) * all.area();
     std::vector<size_t> cand;
     for (size_t k = 0; k < B.prims.size(); ++k)
       if (B.prims[k].box.area() >= lim) cand.push_back(k);

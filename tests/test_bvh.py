@@ -64,9 +64,10 @@ def test_bvh_structure(recs):
     nodes, pairs, big = P.export_bvh()
     kids, parent, leaves = _tree(nodes)
     idx = np.ascontiguousarray(pairs[:, 36:38]).view(np.int32)
-    # the Cornell walls and light (18 large triangles) are the brute-force pre-pass
+    # the Cornell walls and light (18 large triangles) are in the brute-force
+    # pre-pass (with the clutter's cube faces: bvh.cpp kBigFrac), ascending
     bigr = big[big != 0x7FFFFFFF]
-    assert sorted(bigr.tolist()) == list(range(18)) and np.all(np.diff(bigr) > 0)
+    assert set(range(18)) <= set(bigr.tolist()) and len(bigr) <= 32 and np.all(np.diff(bigr) > 0)
     # breadth-first numbering: children come after their parent
     for n in range(len(nodes)):
         for c in range(2):
@@ -280,7 +281,7 @@ def test_quantised_wide_nodes_contain_exact_boxes(name):
     wide, q = P.export_wide()
     assert len(wide) == P.bvh_info()["wide_nodes"] > 0
     if name == "northstar":
-        assert len(q) * 144 <= 32 * 1024 < len(q) * 256  # fits the LDS stage only when quantised
+        assert len(q) * 256 <= 32 * 1024  # the sphere-only tree (cube in the pre-pass) fits the LDS stage
     o = q[:, :3].copy().view(np.float32).astype(np.float64)
     e = np.stack([(q[:, 3] >> (8 * a)) & 0xFF for a in range(3)], 1).astype(np.int64) - 127
     step = np.ldexp(1.0, e)
