@@ -38,6 +38,9 @@ def derive(c, n):
     tri = c["prepass_tri_tests"] + c["shadow_target_tests"] + c["leaf_tri_tests"]
     roots = c["casts"] - c["shadow_decided_before_tree"]
     box = roots + 8 * c["node_visits"]
+    if c["casts"]:  # BVH scene: its culled shadow pre-pass (pair boxes + marked pair tests) too
+        tri += 2 * c["cull_lane_pair_tests"]
+        box += c["cull_lane_box_tests"]
     return {"samples": n, "casts_per_sample": c["casts"] / n, "tri_tests_per_sample": tri / n,
             "box_tests_per_sample": box / n, "flop_per_sample": (38 * tri + 12 * box) / n,
             "tree_rays_per_cast": c["tree_rays"] / max(1, c["casts"]),
