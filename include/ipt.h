@@ -133,7 +133,9 @@ int ipt_scene_export_wide(void *scene, float *wide, uint32_t *qwide);
  * (nullable, n ints): >= 0 marks a next-event shadow ray towards that
  * emitter triangle, for which only "idx == target" and then t are defined
  * (the BVH stops once the target is known to be occluded; small scenes use
- * the megakernel's culled shadow cast, which reports -1 when occluded). */
+ * the megakernel's culled shadow cast, which reports -1 when occluded);
+ * < 0 a path ray through the megakernel's path cast (small scenes: the
+ * culled pair loop).  Without targets small scenes run the full pair loop. */
 int ipt_closest_hit_host(void *scene, int64_t n, const float *origins, const float *dirs, const int32_t *targets,
                          float *t, int32_t *idx);
 int ipt_closest_hit_dev(void *scene, int64_t n, const float *origins_dev, const float *dirs_dev,

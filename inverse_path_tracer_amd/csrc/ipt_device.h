@@ -596,6 +596,7 @@ struct BvhView {
   const f2 *big_e3;         // LDS: the pairs' edge-plane offsets
   int nbig;                 // pairs (<= kSmallPairs)
   const PairBox2 *big_boxes;  // the pairs' acceptance boxes (culled shadow pre-pass)
+  const float *big_lds;       // LDS copy of the pairs + their indices (culled path pre-pass), or nullptr
 };
 constexpr int kStackStride = 256;  // = the megakernel's block size
 constexpr int kBvhDone = (int)0x80000000;
@@ -756,7 +757,9 @@ __device__ __forceinline__ uint32_t pair_box_bits(const PairBox2 *boxes, int nP,
       }
     }
   }
-  return need;
+  // an odd nP's last record has an all-+inf second half, which a ray with
+  // three positive direction components "enters" when bt = inf: not a pair
+  return need & ((1u << nP) - 1u);
 }
 
 // The occlusion part of a culled shadow cast over nP pairs (pair_at(j):
@@ -835,6 +838,54 @@ __device__ __forceinline__ int shadow_hit_pairs_small(const lds_f32 *isect_lds, 
   return bi;
 }
 
+// Path ray of the small-scene loop with per-lane pair culling
+// (IPT_PATH_CULL): a lane tests only the pairs whose acceptance box its ray
+// enters within [kEpsUp, inf) -- no other triangle can accept it (the shadow
+// cull's argument with an unbounded far end) -- in ascending index order with
+// pair_ray's arithmetic and in-order strict accept.  Over a subsequence that
+// still holds every triangle the ray can accept, that is the full loop's hit
+// (the lexicographic minimum of (t, index) over the accepting triangles).
+// The pairs come per lane from the workgroup's LDS copy (nine 16-B reads), so
+// the wave runs the test max-over-lanes(pairs entered) times instead of once
+// per pair: a path ray in a room enters the box of the wall it hits (and, at
+// edges and corners, a neighbour's; crossing an object, its two faces'),
+// whereas the wave's lanes together hit nearly every wall.
+#ifndef IPT_PATH_CULL
+#define IPT_PATH_CULL 1
+#endif
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const f4v lds_f4c;
+__device__ __forceinline__ TriPair load_pair_lds(const lds_f32 *pl, int j) {
+  const lds_f4c *q = (const lds_f4c *)(pl + 36 * j);
+  TriPair T;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const f4v v = q[k];
+    T.f[2 * k][0] = v.x;
+    T.f[2 * k][1] = v.y;
+    T.f[2 * k + 1][0] = v.z;
+    T.f[2 * k + 1][1] = v.w;
+  }
+  return T;
+}
+__device__ __forceinline__ int closest_hit_pairs_culled(const lds_f32 *pairs_lds, const PairBox2 *__restrict__ boxes,
+                                                        int nT, V3 p, V3 d, float &best_t) {
+  float bt = __builtin_inff();
+  int bi = -1;
+  int nP = (nT + 1) >> 1;
+  asm volatile("" : "+s"(nP));
+  asm volatile("" : "+s"(boxes));  // see shadow_hit_pairs_small
+  uint32_t need = pair_box_bits(boxes, nP, p, d, bt);
+  while (need) {  // per lane: the wave loops while any lane has a pair left
+    const int j = __builtin_ctz(need);
+    need &= need - 1u;
+    const TriPair T = load_pair_lds(pairs_lds, j);
+    pair_ray(T, pair_origin(T, p), 2 * j, 2 * j + 1, p, d, bt, bi, ld2(T, 9), ld2(T, 13), ld2(T, 17));
+  }
+  best_t = bt;
+  return bi;
+}
+
 // Both children's boxes of an inner node against [0, bt]: h0/h1 = hit,
 // en0/en1 = entry parameters, c0/c1 = child links.
 __device__ __forceinline__ void bvh_node_test(const BvhView &B, int node, const SlabRay &r, float bt, bool &h0,
@@ -854,6 +905,32 @@ __device__ __forceinline__ void bvh_node_test(const BvhView &B, int node, const 
   c1 = __float_as_int(q3.y);
 }
 
+// The large-triangle pre-pass of a path ray with closest_hit_pairs_culled's
+// per-lane pair culling (boxes: big_boxes; pairs and original indices from
+// the LDS copy big_lds).  From the empty state over ascending original
+// indices the strict in-order accept is the lexicographic minimum, as in
+// bvh_big_pass<false>.
+typedef __attribute__((address_space(3))) const int32_t lds_i32c;
+__device__ __forceinline__ void bvh_big_pass_culled(const BvhView &B, V3 p, V3 d, float &bt, int &bi) {
+  int nP = B.nbig;
+  asm volatile("" : "+s"(nP));
+  const PairBox2 *boxes = B.big_boxes;
+  asm volatile("" : "+s"(boxes));
+  uint32_t need = pair_box_bits(boxes, nP, p, d, bt);
+  const lds_f32 *pl = (const lds_f32 *)B.big_lds;
+  const lds_i32c *il = (const lds_i32c *)(B.big_lds + 36 * nP);
+#ifdef IPT_BVH_STATS
+  atomicAdd(&g_bvh_stats[17], (unsigned long long)nP);  // lane box tests
+  atomicAdd(&g_bvh_stats[8], 2ull * (unsigned long long)__builtin_popcount(need));
+#endif
+  while (need) {
+    const int j = __builtin_ctz(need);
+    need &= need - 1u;
+    const TriPair T = load_pair_lds(pl, j);
+    pair_ray(T, pair_origin(T, p), il[2 * j], il[2 * j + 1], p, d, bt, bi, ld2(T, 9), ld2(T, 13), ld2(T, 17));
+  }
+}
+
 // The part of a cast done before the traversal: the shadow target's own
 // test (target >= 0) and the large-triangle pre-pass.  Returns false when
 // the cast is already decided (shadow target missed or occluded).
@@ -869,7 +946,8 @@ __device__ __forceinline__ bool bvh_prepass(const BvhView &B, V3 p, V3 d, float 
 #endif
 #ifdef IPT_BVH_STATS
   atomicAdd(&g_bvh_stats[7], 1ull);
-  if (!(SHADOW && IPT_SHADOW_CULL)) atomicAdd(&g_bvh_stats[8], 2ull * (unsigned long long)B.nbig);
+  if (!(SHADOW && IPT_SHADOW_CULL) && !(!SHADOW && IPT_PATH_CULL && B.big_lds))
+    atomicAdd(&g_bvh_stats[8], 2ull * (unsigned long long)B.nbig);
   if (SHADOW && IPT_SHADOW_CULL) atomicAdd(&g_bvh_stats[17], (unsigned long long)B.nbig);  // lane box tests
   if (SHADOW) atomicAdd(&g_bvh_stats[9], 1ull);
 #endif
@@ -903,6 +981,8 @@ __device__ __forceinline__ bool bvh_prepass(const BvhView &B, V3 p, V3 d, float 
 #endif
       return false;
     }
+  } else if (!SHADOW && IPT_PATH_CULL && B.big_lds && B.nbig > 0) {
+    bvh_big_pass_culled(B, p, d, bt, bi);
   } else if (B.nbig > 0) {
     bvh_big_pass<SHADOW>(B, p, d, bt, bi);
     if (SHADOW && bi != target) {  // occluded by a large triangle: decided

@@ -164,6 +164,7 @@ struct TraceArgs {
   const float4 *bvh_wide;  // WideNode or QWideNode records (kWideF4 float4 each)
   const TriIsect *bvh_wtris;
   int bvh_wide_lds, coop_stride;
+  int bvh_big_lds;  // culled path pre-pass: the large pairs' LDS copy is built (launch_bvh chooses)
   float root_box[6];
   const TriPair *bvh_big;
   const int32_t *bvh_big_idx;
@@ -488,6 +489,24 @@ __device__ __forceinline__ float small_table_entry(const TriPair *__restrict__ p
 
 // LDS carve-out of the BVH instances: node copy (16-B aligned) + stack.
 __host__ __device__ inline size_t bvh_lds_offset(size_t base) { return (base + 15) & ~(size_t)15; }
+// Bytes of the culled path pre-pass's LDS copy of the large pairs (16-B
+// aligned, 36 floats per pair) and their original indices (2 ints per pair).
+__host__ __device__ inline size_t big_lds_bytes(int nbig) {
+  return IPT_PATH_CULL && nbig > 0 ? 12 + (size_t)nbig * (sizeof(TriPair) + 2 * sizeof(int32_t)) : 0;
+}
+// Fill that copy at `at` (rounded up to 16 B from the LDS base); returns the
+// first float after it.
+__device__ __forceinline__ float *big_lds_copy(const TraceArgs &a, float *at, float *base, int tid, int nthr,
+                                               BvhView &bv) {
+  if (!(IPT_PATH_CULL && a.bvh_nbig > 0 && a.bvh_big_lds)) return at;
+  float *pl = at + ((4 - (int)((at - base) & 3)) & 3);
+  const float *g = reinterpret_cast<const float *>(a.bvh_big);
+  for (int i = tid; i < 36 * a.bvh_nbig; i += nthr) pl[i] = g[i];
+  int32_t *il = reinterpret_cast<int32_t *>(pl + 36 * a.bvh_nbig);
+  for (int i = tid; i < 2 * a.bvh_nbig; i += nthr) il[i] = a.bvh_big_idx[i];
+  bv.big_lds = pl;
+  return at + big_lds_bytes(a.bvh_nbig) / sizeof(float);
+}
 
 template <int MODE, bool SPEC, bool BVH>
 __global__ IPT_TRACE_BOUNDS void trace_kernel(
@@ -568,7 +587,14 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     const float *g = reinterpret_cast<const float *>(isect);
     for (int i = tid; i < 20 * nT; i += nthr) lds_is[i] = g[i];
   }
-  float *lds_rec = a.small_pairs ? lds_is + 20 * nT : lds_e3;
+  // small scenes, culled path cast (IPT_PATH_CULL): a copy of the TriPair
+  // records (16-B aligned after the TriIsect copy), gathered per lane
+  float *lds_pr = lds_is + (a.small_pairs ? 20 * nT : 0);
+  if (a.small_pairs && IPT_PATH_CULL) {
+    const float *g = reinterpret_cast<const float *>(pairs);
+    for (int i = tid; i < 36 * nP; i += nthr) lds_pr[i] = g[i];
+  }
+  float *lds_rec = a.small_pairs ? lds_pr + (IPT_PATH_CULL ? 36 * nP : 0) : lds_e3;
   // Camera-ray ring (RING instances): per wave kRingFields x 64 words after the
   // ADJ records, then the camera origin (3 floats per wave).
   const bool RING = ring_on<MODE, BVH>() && a.use_ring;
@@ -588,6 +614,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   bv.big_e3 = nullptr;
   bv.nbig = 0;
   bv.big_boxes = nullptr;
+  bv.big_lds = nullptr;
   CoopView cv;
   cv.wn = nullptr;
   cv.wn_lds = false;
@@ -624,7 +651,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     bv.big_boxes = a.bvh_big_boxes;
     bv.big_e3 = reinterpret_cast<const f2 *>(be3);
     bv.nbig = a.bvh_nbig;
-    float *after = be3 + 6 * a.bvh_nbig;
+    float *after = big_lds_copy(a, be3 + 6 * a.bvh_nbig, reinterpret_cast<float *>(lds), tid, nthr, bv);
     if (SERVE) {
       srvq = after;
       srvc = reinterpret_cast<int *>(srvq + kQFields * kQSlots);
@@ -862,7 +889,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       }
       coop_cast<false>(cv, qn, p, d, t, hit);
     } else if (active) {
-      hit = cast<BVH>(isect, pairs, e3, nT, bv, p, d, t, -1);
+      if (!BVH && IPT_PATH_CULL && e3)
+        hit = closest_hit_pairs_culled((const lds_f32 *)lds_pr, a.pboxes, nT, p, d, t);
+      else
+        hit = cast<BVH>(isect, pairs, e3, nT, bv, p, d, t, -1);
     }
     PHASE(1)
     const bool vertex = active && hit >= 0;
@@ -1542,6 +1572,8 @@ struct GpuScene {
   int *grad_map = nullptr, *slot_tri = nullptr;  // ADJ hot-set LDS slots (large scenes)
   int grid[16] = {0};       // resident workgroups per (mode, spec, bvh) (0 = not queried)
   size_t grid_lds[16] = {0};
+  size_t pick_base[16] = {0};  // launch_bvh's LDS choice per (mode, spec): base bytes it was made for
+  int pick_opt[16] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 };
 
 #ifdef IPT_PHASE_TIMING
@@ -1768,6 +1800,7 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.bvh_wide = nullptr;
   a.bvh_wtris = nullptr;
   a.bvh_wide_lds = 0;
+  a.bvh_big_lds = 0;
   a.coop_stride = 0;
   for (int k = 0; k < 6; ++k) a.root_box[k] = s->host.bvh_root_box[k];
   a.grad_slots = 0;
@@ -1802,13 +1835,15 @@ static bool use_bvh(const GpuScene *s) {
 // BVH LDS carve-out on top of `base` bytes; fills the args' BVH fields.
 // server: the megakernel's layout (ray queue + a 64-lane stack); else one
 // stack per thread of a 256-thread block (the closest-hit probe).
-static size_t bvh_lds(const GpuScene *s, TraceArgs &a, size_t base, bool server) {
+static size_t bvh_lds(const GpuScene *s, TraceArgs &a, size_t base, bool server, bool stage = true,
+                      bool big_copy = true) {
   const size_t nn = s->host.bvh_nodes.size();
-  a.bvh_lds_nodes = (!kCoop && nn * sizeof(BvhNode) <= (size_t)kBvhLdsNodeBytes) ? (int)nn : 0;
+  a.bvh_lds_nodes = (stage && !kCoop && nn * sizeof(BvhNode) <= (size_t)kBvhLdsNodeBytes) ? (int)nn : 0;
   const size_t nw = s->host.bvh_wide.size();
   a.bvh_wide = s->wide;
   a.bvh_wtris = s->wtris;
-  a.bvh_wide_lds = (kCoop && nw * kWideF4 * sizeof(float4) <= (size_t)kBvhLdsNodeBytes) ? (int)nw : 0;
+  a.bvh_wide_lds = (stage && kCoop && nw * kWideF4 * sizeof(float4) <= (size_t)kBvhLdsNodeBytes) ? (int)nw : 0;
+  a.bvh_big_lds = big_copy && IPT_PATH_CULL ? 1 : 0;
   a.coop_stride = 7 * s->host.bvh_wdepth + 8;
   a.bvh_stack = std::max(1, s->host.bvh_depth);
   a.bvh_nbig = (int)s->host.bvh_big_pairs.size();
@@ -1816,7 +1851,8 @@ static size_t bvh_lds(const GpuScene *s, TraceArgs &a, size_t base, bool server)
   a.bvh_big_idx = s->big_idx;
   a.bvh_big_boxes = s->big_boxes;
   const size_t head = bvh_lds_offset(base) + (size_t)a.bvh_lds_nodes * sizeof(BvhNode) +
-                      (size_t)a.bvh_wide_lds * kWideF4 * sizeof(float4) + (size_t)a.bvh_nbig * 6 * sizeof(float);
+                      (size_t)a.bvh_wide_lds * kWideF4 * sizeof(float4) + (size_t)a.bvh_nbig * 6 * sizeof(float) +
+                      (a.bvh_big_lds ? big_lds_bytes(a.bvh_nbig) : 0);
   if (kCoop) return head + (size_t)(kBlock / 64) * 8 * a.coop_stride * sizeof(uint32_t);
   if (server)
     return head + (size_t)kQFields * kQSlots * sizeof(float) + 8 * sizeof(int) + (size_t)a.bvh_stack * 64 * sizeof(uint32_t);
@@ -1825,7 +1861,8 @@ static size_t bvh_lds(const GpuScene *s, TraceArgs &a, size_t base, bool server)
 
 static size_t table_bytes(const TraceArgs &a) {
   return (a.kd_tables ? (size_t)6 * a.nT * sizeof(float) : 0) +
-         (a.small_pairs ? (size_t)kE3Floats * ((a.nT + 1) / 2) * sizeof(float) + 12 + (size_t)a.nT * sizeof(TriIsect)
+         (a.small_pairs ? (size_t)kE3Floats * ((a.nT + 1) / 2) * sizeof(float) + 12 + (size_t)a.nT * sizeof(TriIsect) +
+                              (IPT_PATH_CULL ? (size_t)((a.nT + 1) / 2) * sizeof(TriPair) : 0)
                         : 0);
 }
 
@@ -1894,6 +1931,43 @@ __global__ __launch_bounds__(kBlock) void kdpi_kernel(const float *__restrict__ 
   if (i < n) out[i] = kd[i] / kPiF;
 }
 
+// BVH instances: the LDS extras (the wide nodes' stage, the large pairs' copy
+// of the culled path pre-pass) are taken only as far as they cost no
+// residency: of the four combinations, the first (most staged) with the most
+// resident workgroups per CU.  North-star adjoint: the tree stage + records +
+// bins sit just under 3 workgroups/CU, and the pair copy would tip it to 2
+// (6.6 -> 7.9 ms).  Cached per scene and instance for the base LDS bytes.
+template <int MODE, bool SPEC>
+static int launch_bvh_pick(GpuScene *s, TraceArgs &a, size_t *lds) {
+  const int slot = MODE * 4 + (SPEC ? 2 : 0);
+  const bool opt[4][2] = {{true, true}, {true, false}, {false, true}, {false, false}};
+  const size_t base = *lds;
+  if (s->pick_opt[slot] < 0 || s->pick_base[slot] != base) {
+    int best = -1, best_per_cu = 0;
+    for (int k = 0; k < 4; ++k) {
+      TraceArgs b = a;
+      const size_t l = bvh_lds(s, b, base, IPT_BVH_SERVER != 0, opt[k][0], opt[k][1]);
+      if (l > 160 * 1024) continue;
+      int per_cu = 0;
+      HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<MODE, SPEC, true>,
+                                                           block_threads<true>(), l));
+      if (per_cu > best_per_cu) {
+        best = k;
+        best_per_cu = per_cu;
+      }
+    }
+    if (best < 0) {
+      gpu_set_error("BVH trace kernel cannot be resident (LDS request too large?)");
+      return -1;
+    }
+    s->pick_opt[slot] = best;
+    s->pick_base[slot] = base;
+  }
+  const int k = s->pick_opt[slot];
+  *lds = bvh_lds(s, a, base, IPT_BVH_SERVER != 0, opt[k][0], opt[k][1]);
+  return 0;
+}
+
 template <int MODE>
 static int launch(GpuScene *s, TraceArgs a, size_t lds, const float *kd_dev, float *out, const float *adj,
                   double *grad, const uint8_t *target, double *edges, hipStream_t st) {
@@ -1917,8 +1991,11 @@ static int launch(GpuScene *s, TraceArgs a, size_t lds, const float *kd_dev, flo
     }
   }
   if (use_bvh(s)) {
-    lds = bvh_lds(s, a, lds, IPT_BVH_SERVER != 0);
-    if (s->has_ks) return launch_inst<MODE, true, true>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
+    if (s->has_ks) {
+      if (launch_bvh_pick<MODE, true>(s, a, &lds)) return -1;
+      return launch_inst<MODE, true, true>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
+    }
+    if (launch_bvh_pick<MODE, false>(s, a, &lds)) return -1;
     return launch_inst<MODE, false, true>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
   }
   if (s->has_ks) return launch_inst<MODE, true, false>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
@@ -2133,8 +2210,9 @@ int gpu_selftest_math(uint64_t n, uint64_t seed, uint64_t *counts_host) {
 // the same LDS staging (small-scene plane offsets, BVH nodes + stack).
 // targets[i] >= 0 makes ray i a shadow ray towards that emitter triangle
 // (the BVH and the small scenes' culled shadow cast then answer only "is the
-// closest hit the target, and at which t"; without targets the brute-force
-// loop returns the full closest hit).  Used by the exactness tests of the
+// closest hit the target, and at which t"); targets[i] < 0 runs the
+// megakernel's path cast (the culled one in small scenes); without targets
+// the brute-force loop returns the full closest hit.  Used by the exactness tests of the
 // BVH and of the shadow cull against the brute-force loop.
 template <bool BVH>
 __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__restrict__ isect,
@@ -2158,9 +2236,14 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
   // the culled shadow cast's LDS copy of the TriIsect records (!BVH, small)
   float *lds_is = lds_e3 + kE3Floats * nP;
   lds_is += (4 - (int)((lds_is - lds_e3) & 3)) & 3;
+  float *lds_pr = lds_is + 20 * nT;  // the culled path cast's TriPair copy (!BVH, small)
   if (!BVH && small) {
     const float *g = reinterpret_cast<const float *>(isect);
     for (int i = tid; i < 20 * nT; i += kBlock) lds_is[i] = g[i];
+    if (IPT_PATH_CULL) {
+      const float *gp = reinterpret_cast<const float *>(pairs);
+      for (int i = tid; i < 36 * nP; i += kBlock) lds_pr[i] = gp[i];
+    }
   }
   BvhView bv;
   bv.nodes = bnodes;
@@ -2173,6 +2256,7 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
   bv.big_e3 = nullptr;
   bv.nbig = 0;
   bv.big_boxes = nullptr;
+  bv.big_lds = nullptr;
   CoopView cv;
   cv.wn = a.bvh_wide;
   cv.wn_lds = false;
@@ -2204,7 +2288,8 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
     bv.big_boxes = a.bvh_big_boxes;
     bv.big_e3 = reinterpret_cast<const f2 *>(be3);
     bv.nbig = a.bvh_nbig;
-    uint32_t *after = reinterpret_cast<uint32_t *>(be3 + 6 * a.bvh_nbig);
+    uint32_t *after = reinterpret_cast<uint32_t *>(
+        big_lds_copy(a, be3 + 6 * a.bvh_nbig, reinterpret_cast<float *>(lds), tid, kBlock, bv));
     if (kCoop) cv.stk = after + (tid >> 6) * 8 * a.coop_stride;
     else bv.stack = after + tid;
   }
@@ -2235,6 +2320,8 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
   } else if (valid) {
     if (!BVH && IPT_SHADOW_CULL && small && target >= 0)  // the megakernel's shadow cast of small scenes
       h = shadow_hit_pairs_small((const lds_f32 *)lds_is, pairs, a.pboxes, e3, nT, p, d, target, t);
+    else if (!BVH && IPT_PATH_CULL && small && targets && target < 0)  // ... and its path cast
+      h = closest_hit_pairs_culled((const lds_f32 *)lds_pr, a.pboxes, nT, p, d, t);
     else
       h = cast<BVH>(isect, pairs, e3, nT, bv, p, d, t, target);
   }
@@ -2274,7 +2361,9 @@ int gpu_closest_hit(GpuScene *s, int64_t n, const float *org_dev, const float *d
     hipLaunchKernelGGL(closest_hit_kernel<true>, dim3(blocks), dim3(kBlock), lds, (hipStream_t)stream, s->isect,
                        s->pairs, s->bnodes, s->bpairs, a, small, n, org_dev, dir_dev, targets_dev, t_dev, idx_dev);
   } else {
-    const size_t lds = base + (small ? 12 + (size_t)s->host.nT * sizeof(TriIsect) : 0);
+    const size_t lds = base + (small ? 12 + (size_t)s->host.nT * sizeof(TriIsect) +
+                                           (IPT_PATH_CULL ? (size_t)((s->host.nT + 1) / 2) * sizeof(TriPair) : 0)
+                                     : 0);
     hipLaunchKernelGGL(closest_hit_kernel<false>, dim3(blocks), dim3(kBlock), lds, (hipStream_t)stream, s->isect,
                        s->pairs, s->bnodes, s->bpairs, a, small, n, org_dev, dir_dev, targets_dev, t_dev, idx_dev);
   }

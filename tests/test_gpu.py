@@ -560,3 +560,45 @@ def test_culled_shadow_query_equals_brute_force(which):
     assert 0.05 < vis_f.mean() < 0.98
     assert np.array_equal(bits(tc[vis_c]), bits(tf[vis_f]))
     P.close()
+
+
+@pytest.mark.parametrize("which", ["cornell", "scene0"])
+def test_culled_path_cast_equals_brute_force(oracle, which):
+    """Small scenes: the megakernel's culled path cast (a lane tests only the
+    pairs whose acceptance box its ray enters, per-lane from the LDS copy)
+    returns the full brute-force loop's hit bit-for-bit (index and t), and the
+    oracle's: rays from points on every triangle in all directions (grazing
+    included), adversarial rays at vertices and edges from the camera, and
+    random rays inside the scene box."""
+    recs = CORNELL if which == "cornell" else SCENE0
+    P = product_scene(recs)
+    tris = P.triangles()
+    rng = np.random.RandomState(31)
+    n = 300000
+    v = tris[:, 0:9].reshape(-1, 3, 3)
+    src = rng.randint(0, P.nT, n)
+    a, b = rng.uniform(0, 1, (2, n))
+    flip = a + b > 1
+    a[flip], b[flip] = 1 - a[flip], 1 - b[flip]
+    O = v[src, 0] + a[:, None] * (v[src, 1] - v[src, 0]) + b[:, None] * (v[src, 2] - v[src, 0])
+    D = rng.normal(size=(n, 3))
+    nrm = np.cross(v[src, 1] - v[src, 0], v[src, 2] - v[src, 0])
+    graze = rng.uniform(0, 1, n) < 0.2  # directions within ~1e-3 of the triangle's plane
+    Dg = D - (np.sum(D * nrm, 1) / np.sum(nrm * nrm, 1))[:, None] * nrm
+    D[graze] = Dg[graze] + rng.normal(0, 1e-3, (int(graze.sum()), 3))
+    D /= np.linalg.norm(D, axis=1, keepdims=True)
+    Oa, Da = _rays(P, 20000, 60000, 5)
+    O = np.concatenate([O.astype(np.float32), Oa])
+    D = np.concatenate([D.astype(np.float32), Da])
+    tg = np.full(len(O), -1, np.int32)
+    tc, ic = P.closest_hit(O, D, targets=tg)
+    tf, i_f = P.closest_hit(O, D)
+    assert np.array_equal(ic, i_f)
+    assert np.array_equal(bits(tc), bits(tf))
+    assert (ic >= 0).mean() > 0.4  # the Cornell box is open at the front
+    Q = oracle.OracleScene(recs)
+    tq, iq = Q.closest_hit(O[:60000], D[:60000])
+    assert np.array_equal(iq, ic[:60000])
+    hit = iq >= 0
+    assert np.array_equal(bits(tq[hit]), bits(tc[:60000][hit]))
+    P.close()
