@@ -74,10 +74,11 @@ BVH_STATS_FILE = os.path.join(ROOT, "profiles", "bvh_stats.json")
 
 
 def executed_flop_per_sample(name, c_bar, n_tri):
-    """Small scenes: the tests the culled shadow cast actually executes
-    (profiles/bvh_stats.json, IPT_BVH_STATS build): path casts x nT + the
-    shadow casts' target tests and the pair tests some lane needed, x 38,
-    plus 12 per slab (box) test.  None without the stats file."""
+    """Small scenes: the tests the culled casts actually execute
+    (profiles/bvh_stats.json, IPT_BVH_STATS build): the path casts' pair
+    tests of the pairs each lane's ray enters, the shadow casts' target tests
+    and the pair tests some lane needed, x 38, plus 12 per slab (box) test.
+    None without the stats file."""
     if not os.path.exists(BVH_STATS_FILE):
         return None
     with open(BVH_STATS_FILE) as f:
@@ -85,8 +86,11 @@ def executed_flop_per_sample(name, c_bar, n_tri):
     d = st.get(name + "_fwd", {}).get("derived")
     if not d or "cull_shadow_casts_per_sample" not in d:
         return None
-    path = c_bar - d["cull_shadow_casts_per_sample"]
-    return 38 * (path * n_tri + d["cull_tri_tests_per_sample"]) + 12 * d["cull_box_tests_per_sample"]
+    if d.get("pcull_casts_per_sample"):  # culled path casts: the pair tests and box tests they issue
+        path_flop = 38 * d["pcull_tri_tests_per_sample"] + 12 * d["pcull_box_tests_per_sample"]
+    else:
+        path_flop = 38 * (c_bar - d["cull_shadow_casts_per_sample"]) * n_tri
+    return path_flop + 38 * d["cull_tri_tests_per_sample"] + 12 * d["cull_box_tests_per_sample"]
 
 
 def flop_per_sample(key):

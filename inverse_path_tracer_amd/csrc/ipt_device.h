@@ -607,7 +607,7 @@ constexpr int kBvhDone = (int)0x80000000;
 // triangle tests, [5] coop calls with >= 1 ray (per wave), [6] coop rounds
 // (per wave); pre-pass: [7] casts, [8] large-triangle tests, [9] shadow
 // target tests, [10] shadow rays decided before the tree.
-constexpr int kBvhStats = 18;  // [12..17]: culled shadow casts (shadow_hit_pairs_small)
+constexpr int kBvhStats = 21;  // [12..17]: culled shadow casts (shadow_hit_pairs_small); [18..20]: culled path casts
 #ifdef IPT_BVH_STATS
 __device__ unsigned long long g_bvh_stats[kBvhStats];
 #endif
@@ -876,6 +876,11 @@ __device__ __forceinline__ int closest_hit_pairs_culled(const lds_f32 *pairs_lds
   asm volatile("" : "+s"(nP));
   asm volatile("" : "+s"(boxes));  // see shadow_hit_pairs_small
   uint32_t need = pair_box_bits(boxes, nP, p, d, bt);
+#ifdef IPT_BVH_STATS
+  atomicAdd(&g_bvh_stats[18], 1ull);                                            // path casts
+  atomicAdd(&g_bvh_stats[19], (unsigned long long)__builtin_popcount(need));    // lane pair tests
+  atomicAdd(&g_bvh_stats[20], (unsigned long long)nP);                          // lane box tests
+#endif
   while (need) {  // per lane: the wave loops while any lane has a pair left
     const int j = __builtin_ctz(need);
     need &= need - 1u;

@@ -31,7 +31,7 @@ from inverse_path_tracer_amd.scene import ObjectSpec, Scene  # noqa: E402
 NAMES = ["tree_rays", "node_visits", "leaf_visits", "shadow_occluded_in_tree", "leaf_tri_tests", "coop_calls",
          "coop_rounds", "casts", "prepass_tri_tests", "shadow_target_tests", "shadow_decided_before_tree", "unused",
          "cull_shadow_lanes", "cull_target_accepted", "cull_wave_calls", "cull_wave_pair_tests",
-         "cull_lane_pair_tests", "cull_lane_box_tests"]
+         "cull_lane_pair_tests", "cull_lane_box_tests", "pcull_casts", "pcull_lane_pair_tests", "pcull_lane_box_tests"]
 
 
 def derive(c, n):
@@ -53,7 +53,11 @@ def derive(c, n):
             "cull_pairs_tested_per_wave_call": c["cull_wave_pair_tests"] / max(1, c["cull_wave_calls"]),
             "cull_shadow_casts_per_sample": c["cull_shadow_lanes"] / n,
             "cull_tri_tests_per_sample": (c["cull_shadow_lanes"] + 2 * c["cull_lane_pair_tests"]) / n,
-            "cull_box_tests_per_sample": c["cull_lane_box_tests"] / n}
+            "cull_box_tests_per_sample": c["cull_lane_box_tests"] / n,
+            "pcull_casts_per_sample": c.get("pcull_casts", 0) / n,
+            "pcull_tri_tests_per_sample": 2 * c.get("pcull_lane_pair_tests", 0) / n,
+            "pcull_pairs_per_cast": c.get("pcull_lane_pair_tests", 0) / max(1, c.get("pcull_casts", 0)),
+            "pcull_box_tests_per_sample": c.get("pcull_lane_box_tests", 0) / n}
 
 
 def main():
