@@ -128,6 +128,11 @@ int ipt_scene_export_bvh(void *scene, float *nodes, float *pairs, int32_t *big_i
  * pad), qwide info8[5]*36 uint32 (QWideNode: origin xyz float bits, step
  * exponent bytes, per child packed 8-bit bounds, ref, 0); each nullable. */
 int ipt_scene_export_wide(void *scene, float *wide, uint32_t *qwide);
+/* The shadow rays' potential occluders (bvh.cpp shadow_occluder_masks):
+ * masks receives nT * max(nE, 1) words, word [s * nE + e] = the pairs (bit j
+ * = triangles 2j, 2j+1) that may occlude a shadow ray from a vertex on
+ * triangle s to a point on emitter e (all pairs when not bounded). */
+int ipt_scene_shadow_masks(void *scene, uint32_t *masks);
 /* Closest hit of n rays (origins, dirs: n*3 floats) through the kernels'
  * own cast: idx = triangle index or -1, t = its distance.  targets
  * (nullable, n ints): >= 0 marks a next-event shadow ray towards that
@@ -140,6 +145,13 @@ int ipt_closest_hit_host(void *scene, int64_t n, const float *origins, const flo
                          float *t, int32_t *idx);
 int ipt_closest_hit_dev(void *scene, int64_t n, const float *origins_dev, const float *dirs_dev,
                         const int32_t *targets_dev, float *t_dev, int32_t *idx_dev, void *stream);
+/* Shadow rays exactly as the megakernel casts them from a path vertex:
+ * sources[i] >= 0 is the triangle the origin lies on (its vertex), which in
+ * small scenes selects the static potential-occluder mask of (source,
+ * emitter) on top of the culled shadow cast; < 0 = no mask.  targets[i] >= 0
+ * as in ipt_closest_hit_host (both arrays required). */
+int ipt_shadow_hit_host(void *scene, int64_t n, const float *origins, const float *dirs, const int32_t *targets,
+                        const int32_t *sources, float *t, int32_t *idx);
 
 /* Host-memory entry points (synchronous). */
 int ipt_render_samples_host(void *scene, const ipt_params_t *p, float *samples); /* rows*W*spp*3 */

@@ -106,6 +106,9 @@ SIGNATURES = {
     "ipt_scene_export_wide": (C.c_int, [vp, fp, C.POINTER(C.c_uint32)]),
     "ipt_closest_hit_host": (C.c_int, [vp, C.c_int64, fp, fp, C.POINTER(C.c_int32), fp, C.POINTER(C.c_int32)]),
     "ipt_closest_hit_dev": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp, vp, vp]),
+    "ipt_scene_shadow_masks": (C.c_int, [vp, C.POINTER(C.c_uint32)]),
+    "ipt_shadow_hit_host": (C.c_int, [vp, C.c_int64, fp, fp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), fp,
+                                      C.POINTER(C.c_int32)]),
     "ipt_png_write": (C.c_int, [C.c_char_p, C.c_int, C.c_int, u8p]),
     "ipt_png_read": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), u8p, C.c_int64]),
 }

@@ -322,6 +322,113 @@ std::vector<PairBox2> pair_boxes(const HostScene &S) {
   return out;
 }
 
+// Potential occluders of next-event shadow rays, per (source triangle S,
+// emitter e): bit j = pair j might accept a shadow ray from a vertex on S to
+// a point on emitter triangle E = emit_tri[e].  Every such ray has its origin
+// p in S's acceptance box (p is the point S's test accepted), its target pt
+// in E's vertex box (padded), d = unit(pt - p) within 2^-21 relative, and
+// only t in [1e-2, t_E (1 + tiny)] matters.  A triangle w accepts only points
+// q with |n_w.q - n_w.c_w| <= h (acceptance_box), and a computed q lies
+// within eps << 2^-14 R of the exact line point p + t d.  Along the segment,
+// f(x) = n_w.x - n_w.c_w = (1 - s) f(p) + s f(pt), s = t / |pt - p| in
+// [1e-2 / L_max, 1]: affine in s, so when f keeps one sign with margin
+// h + eps at both ends for every p and pt (box corners bound f), w cannot
+// accept.  A pair is left out only if both its triangles are.  The emitter's
+// own pair (coplanar partner) always stays; in a room, a wall on whose plane
+// S ends (a neighbour) is left out thanks to the 1e-2 lower end.
+std::vector<uint32_t> shadow_occluder_masks(const HostScene &S) {
+  const int nT = S.nT, nE = S.nE, nP = (nT + 1) / 2;
+  const uint32_t all = nP >= 32 ? 0xffffffffu : ((1u << nP) - 1u);
+  std::vector<uint32_t> out((size_t)nT * (size_t)std::max(nE, 1), all);
+  if (nP > 32 || nE == 0) return out;
+  const double r_all = scene_coord_bound(S);
+  const double h = std::ldexp(3.0 * r_all, -17), thr = h + std::ldexp(r_all, -14);
+  struct B3 {
+    double lo[3], hi[3];
+    bool ok;
+  };
+  std::vector<B3> src((size_t)nT);
+  for (int i = 0; i < nT; ++i) {
+    float l[3], u[3];
+    src[(size_t)i].ok = acceptance_box(S.isect[(size_t)i], S.geom[(size_t)i], r_all, l, u) == 0;
+    for (int a = 0; a < 3; ++a) {
+      src[(size_t)i].lo[a] = l[a];
+      src[(size_t)i].hi[a] = u[a];
+    }
+  }
+  auto corners = [](const B3 &b, int k, double x[3]) {
+    for (int a = 0; a < 3; ++a) x[a] = (k >> a) & 1 ? b.hi[a] : b.lo[a];
+  };
+  for (int e = 0; e < nE; ++e) {
+    const int et = S.emit_tri[(size_t)e];
+    B3 E;
+    E.ok = true;
+    const double pad = std::ldexp(r_all, -18);
+    for (int a = 0; a < 3; ++a) {
+      E.lo[a] = HUGE_VAL;
+      E.hi[a] = -HUGE_VAL;
+      for (int j = 0; j < 3; ++j) {
+        E.lo[a] = std::min(E.lo[a], (double)S.geom[(size_t)et].v[j][a]);
+        E.hi[a] = std::max(E.hi[a], (double)S.geom[(size_t)et].v[j][a]);
+      }
+      E.lo[a] -= pad;
+      E.hi[a] += pad;
+    }
+    for (int si = 0; si < nT; ++si) {
+      const B3 &Sb = src[(size_t)si];
+      if (!Sb.ok) continue;  // unbounded (or never accepted): every pair stays
+      double lmax = 0.0;
+      for (int k = 0; k < 8; ++k)
+        for (int m = 0; m < 8; ++m) {
+          double x[3], y[3];
+          corners(Sb, k, x);
+          corners(E, m, y);
+          lmax = std::max(lmax, std::sqrt((x[0] - y[0]) * (x[0] - y[0]) + (x[1] - y[1]) * (x[1] - y[1]) +
+                                          (x[2] - y[2]) * (x[2] - y[2])));
+        }
+      const double slo = 0.01 / (lmax * (1.0 + 1e-6) + 1e-30);
+      uint32_t mask = 0;
+      for (int j = 0; j < nP; ++j) {
+        bool excluded = true;
+        for (int hh = 0; hh < 2 && excluded; ++hh) {
+          const int w = 2 * j + hh;
+          if (w >= nT) continue;  // the padding triangle is never accepted
+          const TriIsect &T = S.isect[(size_t)w];
+          const double n[3] = {T.n[0], T.n[1], T.n[2]};
+          if (n[0] == 0.0 && n[1] == 0.0 && n[2] == 0.0) continue;  // never accepted
+          bool finite = true;
+          for (int a = 0; a < 3; ++a) finite = finite && std::isfinite(n[a]) && std::isfinite(T.c[a]);
+          if (!finite) {
+            excluded = false;
+            break;
+          }
+          const double nc = n[0] * T.c[0] + n[1] * T.c[1] + n[2] * T.c[2];
+          auto frange = [&](const B3 &b, double &mn, double &mx) {
+            mn = HUGE_VAL;
+            mx = -HUGE_VAL;
+            for (int k = 0; k < 8; ++k) {
+              double x[3];
+              corners(b, k, x);
+              const double f = n[0] * x[0] + n[1] * x[1] + n[2] * x[2] - nc;
+              mn = std::min(mn, f);
+              mx = std::max(mx, f);
+            }
+          };
+          double aS, AS, aE, AE;
+          frange(Sb, aS, AS);
+          frange(E, aE, AE);
+          const bool pos = aE > thr && (1.0 - slo) * aS + slo * aE > thr;
+          const bool neg = AE < -thr && (1.0 - slo) * AS + slo * AE < -thr;
+          if (!(pos || neg)) excluded = false;
+        }
+        if (!excluded) mask |= 1u << j;
+      }
+      out[(size_t)si * nE + e] = mask;
+    }
+  }
+  return out;
+}
+
 // Collapse the binary tree into 8-wide nodes: starting from a binary node's
 // two children, repeatedly open the inner child with the largest box until
 // the node has 8 children or only leaves remain.  Leaves keep their binary

@@ -29,5 +29,8 @@ double scene_coord_bound(const HostScene &S);
 // per record (scene_layout.h PairBox2), for the culled shadow cast of small
 // scenes (ipt_device.h::shadow_hit_pairs_small).
 std::vector<PairBox2> pair_boxes(const HostScene &S);
+// Per (source triangle, emitter): the pairs that might occlude a shadow ray
+// (bit j = pair j), nT * nE words; see bvh.cpp.
+std::vector<uint32_t> shadow_occluder_masks(const HostScene &S);
 
 }  // namespace ipt

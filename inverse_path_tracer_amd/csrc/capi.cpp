@@ -11,6 +11,7 @@
 #include "gpu_api.h"
 #include "png_io.h"
 #include "scene_io.h"
+#include "bvh.h"
 
 using ipt::GpuScene;
 
@@ -223,6 +224,13 @@ int ipt_scene_export_wide(void *scene, float *wide, uint32_t *qwide) {
     std::memcpy(qwide, h.bvh_qwide.data(), h.bvh_qwide.size() * sizeof(ipt::QWideNode));
   return 0;
 }
+int ipt_scene_shadow_masks(void *scene, uint32_t *masks) {
+  GpuScene *s = as_scene(scene);
+  if (!s || !masks) return -1;
+  const std::vector<uint32_t> m = ipt::shadow_occluder_masks(ipt::gpu_host(s));
+  std::memcpy(masks, m.data(), m.size() * sizeof(uint32_t));
+  return 0;
+}
 int ipt_scene_set_accel(void *scene, int mode) {
   GpuScene *s = as_scene(scene);
   if (!s) return -1;
@@ -235,13 +243,22 @@ int ipt_closest_hit_host(void *scene, int64_t n, const float *origins, const flo
     if (s) fail("ipt_closest_hit_host: bad arguments");
     return -1;
   }
-  return gpu_status(ipt::gpu_closest_hit_host(s, n, origins, dirs, targets, t, idx));
+  return gpu_status(ipt::gpu_closest_hit_host(s, n, origins, dirs, targets, nullptr, t, idx));
+}
+int ipt_shadow_hit_host(void *scene, int64_t n, const float *origins, const float *dirs, const int32_t *targets,
+                        const int32_t *sources, float *t, int32_t *idx) {
+  GpuScene *s = as_scene(scene);
+  if (!s || n < 0 || (n > 0 && (!origins || !dirs || !targets || !sources || !t || !idx))) {
+    if (s) fail("ipt_shadow_hit_host: bad arguments");
+    return -1;
+  }
+  return gpu_status(ipt::gpu_closest_hit_host(s, n, origins, dirs, targets, sources, t, idx));
 }
 int ipt_closest_hit_dev(void *scene, int64_t n, const float *origins_dev, const float *dirs_dev,
                         const int32_t *targets_dev, float *t_dev, int32_t *idx_dev, void *stream) {
   GpuScene *s = as_scene(scene);
   if (!s || n < 0) return -1;
-  return gpu_status(ipt::gpu_closest_hit(s, n, origins_dev, dirs_dev, targets_dev, t_dev, idx_dev, stream));
+  return gpu_status(ipt::gpu_closest_hit(s, n, origins_dev, dirs_dev, targets_dev, nullptr, t_dev, idx_dev, stream));
 }
 
 int ipt_scene_get_materials(void *scene, float *kd) {

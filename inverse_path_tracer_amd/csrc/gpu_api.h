@@ -49,11 +49,12 @@ int gpu_graph_host(GpuScene *s, const RenderParams &p, const uint8_t *target, do
 int gpu_set_accel(GpuScene *s, int mode);
 int gpu_accel_in_use(const GpuScene *s);
 // Closest hit of n caller-supplied rays (origins, directions: n*3 floats;
-// targets: nullable, n ints, >= 0 = shadow ray towards that emitter).
+// targets: nullable, n ints, >= 0 = shadow ray towards that emitter;
+// sources: nullable, n ints, >= 0 = the shadow ray starts on that triangle).
 int gpu_closest_hit(GpuScene *s, int64_t n, const float *org_dev, const float *dir_dev, const int *targets_dev,
-                    float *t_dev, int *idx_dev, void *stream);
-int gpu_closest_hit_host(GpuScene *s, int64_t n, const float *org, const float *dir, const int *targets, float *t,
-                         int *idx);
+                    const int *sources_dev, float *t_dev, int *idx_dev, void *stream);
+int gpu_closest_hit_host(GpuScene *s, int64_t n, const float *org, const float *dir, const int *targets,
+                         const int *sources, float *t, int *idx);
 
 int gpu_device_count();
 int gpu_selftest_math(uint64_t n, uint64_t seed, uint64_t *counts);  // 8 mismatch counters

@@ -736,14 +736,25 @@ __device__ __forceinline__ SlabRay slab_ray(V3 p, V3 d) {
 #ifndef IPT_SHADOW_CULL
 #define IPT_SHADOW_CULL 1
 #endif
+// IPT_SHADOW_PO=1: the culled shadow cast also skips, per lane, the pairs
+// that cannot occlude any shadow ray from its vertex's triangle to its
+// emitter (static potential-occluder masks, bvh.cpp shadow_occluder_masks)
+#ifndef IPT_SHADOW_PO
+#define IPT_SHADOW_PO 1
+#endif
+typedef __attribute__((address_space(3))) const uint32_t lds_u32c;
 // Bit j: the ray enters pair j's acceptance box within [kEpsUp, bt] (the
 // pairs' boxes two per PairBox2 record; scalar loads).
-__device__ __forceinline__ uint32_t pair_box_bits(const PairBox2 *boxes, int nP, V3 p, V3 d, float bt) {
+// allow: the pairs this lane may need at all (shadow rays: the potential
+// occluders of its (source triangle, emitter), bvh.cpp
+// shadow_occluder_masks); a record no lane allows is skipped by the wave.
+__device__ __forceinline__ uint32_t pair_box_bits(const PairBox2 *boxes, int nP, V3 p, V3 d, float bt,
+                                                  uint32_t allow = 0xffffffffu) {
   uint32_t need = 0;
   const SlabRay r = slab_ray(p, d);
 #pragma unroll
   for (int J = 0; J < kSmallPairs / 2; ++J) {
-    if (2 * J < nP) {  // wave-uniform
+    if (2 * J < nP && __builtin_amdgcn_ballot_w64((allow >> (2 * J)) & 3u)) {  // wave-uniform
       const cst_f32 *B = (const cst_f32 *)(boxes + J);
       const f2 tx0 = fma2(f2{B[0], B[1]}, r.ix, r.ox), tx1 = fma2(f2{B[2], B[3]}, r.ix, r.ox);
       const f2 ty0 = fma2(f2{B[4], B[5]}, r.iy, r.oy), ty1 = fma2(f2{B[6], B[7]}, r.iy, r.oy);
@@ -759,7 +770,7 @@ __device__ __forceinline__ uint32_t pair_box_bits(const PairBox2 *boxes, int nP,
   }
   // an odd nP's last record has an all-+inf second half, which a ray with
   // three positive direction components "enters" when bt = inf: not a pair
-  return need & ((1u << nP) - 1u);
+  return need & allow & ((1u << nP) - 1u);
 }
 
 // The occlusion part of a culled shadow cast over nP pairs (pair_at(j):
@@ -801,7 +812,7 @@ __device__ __forceinline__ bool occlusion_pass(PairAt pair_at, IdxAt idx_at, lds
 
 __device__ __forceinline__ int shadow_hit_pairs_small(const lds_f32 *isect_lds, const TriPair *__restrict__ pairs,
                                                       const PairBox2 *__restrict__ boxes, const f2 *e3, int nT, V3 p,
-                                                      V3 d, int target, float &best_t) {
+                                                      V3 d, int target, float &best_t, uint32_t allow = 0xffffffffu) {
   float bt = __builtin_inff();
   int bi = -1;
   {  // the target's record from the LDS copy of the TriIsect array
@@ -829,7 +840,7 @@ __device__ __forceinline__ int shadow_hit_pairs_small(const lds_f32 *isect_lds, 
   asm volatile("" : "+s"(boxes));
   if (__builtin_amdgcn_ballot_w64(live)) {
     // box bits first, so that the slab registers are dead before the pair tests
-    const uint32_t need = pair_box_bits(boxes, nP, p, d, bt);
+    const uint32_t need = pair_box_bits(boxes, nP, p, d, bt, live ? allow : 0u);
     live = occlusion_pass([&](int j) { return pairs[j]; }, [&](int k) { return k; }, e3l, nP, need, p, d, target, bt,
                           live);
     if (!live && bi >= 0) bi = -1;  // occluded: not the target (the caller only compares with it)

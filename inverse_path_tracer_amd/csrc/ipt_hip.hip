@@ -201,6 +201,9 @@ struct TraceArgs {
   uint32_t *chunk_ctr;
   // small scenes: acceptance boxes of the pairs (culled shadow casts)
   const PairBox2 *pboxes;
+  // small scenes: potential occluders per (source triangle, emitter), nT*nE
+  // words (bvh.cpp shadow_occluder_masks), copied to LDS; nullptr = none
+  const uint32_t *pomask;
 };
 static_assert(alignof(TraceArgs) == 8, "TraceArgs sits right after the ten 8-B scene pointers in the kernarg segment");
 
@@ -594,7 +597,12 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     const float *g = reinterpret_cast<const float *>(pairs);
     for (int i = tid; i < 36 * nP; i += nthr) lds_pr[i] = g[i];
   }
-  float *lds_rec = a.small_pairs ? lds_pr + (IPT_PATH_CULL ? 36 * nP : 0) : lds_e3;
+  // ... and the shadow casts' potential-occluder masks (IPT_SHADOW_PO)
+  uint32_t *lds_po = reinterpret_cast<uint32_t *>(lds_pr + (a.small_pairs && IPT_PATH_CULL ? 36 * nP : 0));
+  const bool po = a.small_pairs && IPT_SHADOW_PO && a.pomask;
+  if (po)
+    for (int i = tid; i < nT * nE; i += nthr) lds_po[i] = a.pomask[i];
+  float *lds_rec = a.small_pairs ? reinterpret_cast<float *>(lds_po) + (po ? nT * nE : 0) : lds_e3;
   // Camera-ray ring (RING instances): per wave kRingFields x 64 words after the
   // ADJ records, then the camera origin (3 floats per wave).
   const bool RING = ring_on<MODE, BVH>() && a.use_ring;
@@ -1018,7 +1026,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         coop_cast<true>(cv, qn, p, sd, ts, hs);
       } else if (!SERVE && shadow) {
         if (!BVH && IPT_SHADOW_CULL && e3)
-          hs = shadow_hit_pairs_small((const lds_f32 *)lds_is, pairs, a.pboxes, e3, nT, p, sd, et, ts);
+          hs = shadow_hit_pairs_small((const lds_f32 *)lds_is, pairs, a.pboxes, e3, nT, p, sd, et, ts,
+                                      po ? ((const lds_u32c *)lds_po)[tri * nE + emitter] : 0xffffffffu);
         else
           hs = cast<BVH>(isect, pairs, e3, nT, bv, p, sd, ts, et);
       }
@@ -1568,6 +1577,7 @@ struct GpuScene {
   float4 *wide = nullptr;  // WideNode or QWideNode records (IPT_BVH_QNODES)
   TriIsect *wtris = nullptr;
   PairBox2 *pboxes = nullptr;  // pair acceptance boxes (small scenes' culled shadow casts)
+  uint32_t *pomask = nullptr;  // shadow rays' potential occluders (small scenes)
   int accel = IPT_ACCEL_AUTO;
   int *grad_map = nullptr, *slot_tri = nullptr;  // ADJ hot-set LDS slots (large scenes)
   int grid[16] = {0};       // resident workgroups per (mode, spec, bvh) (0 = not queried)
@@ -1628,7 +1638,8 @@ GpuScene *gpu_upload(const HostScene &host, std::string *err) {
       upload(&s->big_pairs, host.bvh_big_pairs) || upload(&s->big_idx, host.bvh_big_idx) ||
       upload(&s->big_boxes, host.bvh_big_boxes) ||
       (IPT_BVH_QNODES ? upload_as_f4(&s->wide, host.bvh_qwide) : upload_as_f4(&s->wide, host.bvh_wide)) ||
-      upload(&s->wtris, host.bvh_wtris) || upload(&s->pboxes, pair_boxes(host))) {
+      upload(&s->wtris, host.bvh_wtris) || upload(&s->pboxes, pair_boxes(host)) ||
+      upload(&s->pomask, shadow_occluder_masks(host))) {
     *err = gpu_last_error();
     gpu_free(s);
     return nullptr;
@@ -1692,6 +1703,7 @@ void gpu_free(GpuScene *s) {
   (void)hipFree(s->wide);
   (void)hipFree(s->wtris);
   (void)hipFree(s->pboxes);
+  (void)hipFree(s->pomask);
   (void)hipFree(s->grad_map);
   (void)hipFree(s->slot_tri);
   delete s;
@@ -1812,6 +1824,7 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.chunk = 0;
   a.chunk_ctr = nullptr;
   a.pboxes = s->pboxes;
+  a.pomask = s->host.nE > 0 ? s->pomask : nullptr;
   a.nscenes = p.nscenes > 1 ? p.nscenes : 1;
   a.bps = 1;
   a.seed_stride = p.seed_stride;
@@ -1862,7 +1875,8 @@ static size_t bvh_lds(const GpuScene *s, TraceArgs &a, size_t base, bool server,
 static size_t table_bytes(const TraceArgs &a) {
   return (a.kd_tables ? (size_t)6 * a.nT * sizeof(float) : 0) +
          (a.small_pairs ? (size_t)kE3Floats * ((a.nT + 1) / 2) * sizeof(float) + 12 + (size_t)a.nT * sizeof(TriIsect) +
-                              (IPT_PATH_CULL ? (size_t)((a.nT + 1) / 2) * sizeof(TriPair) : 0)
+                              (IPT_PATH_CULL ? (size_t)((a.nT + 1) / 2) * sizeof(TriPair) : 0) +
+                              (IPT_SHADOW_PO && a.pomask ? (size_t)a.nT * a.nE * sizeof(uint32_t) : 0)
                         : 0);
 }
 
@@ -2221,7 +2235,9 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
                                                              const BvhPair *__restrict__ bpairs, const TraceArgs a,
                                                              int small, int64_t n, const float *__restrict__ org,
                                                              const float *__restrict__ dir,
-                                                             const int *__restrict__ targets, float *__restrict__ t_out,
+                                                             const int *__restrict__ targets,
+                                                             const int *__restrict__ sources,
+                                                             const int *__restrict__ emit_tri, float *__restrict__ t_out,
                                                              int *__restrict__ i_out) {
   extern __shared__ double lds[];
   const int tid = threadIdx.x;
@@ -2318,8 +2334,15 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
     coop_cast<false>(cv, qn && target < 0, p, d, t, h);
     coop_cast<true>(cv, qn && target >= 0, p, d, t, h);
   } else if (valid) {
-    if (!BVH && IPT_SHADOW_CULL && small && target >= 0)  // the megakernel's shadow cast of small scenes
-      h = shadow_hit_pairs_small((const lds_f32 *)lds_is, pairs, a.pboxes, e3, nT, p, d, target, t);
+    if (!BVH && IPT_SHADOW_CULL && small && target >= 0) {  // the megakernel's shadow cast of small scenes
+      uint32_t allow = 0xffffffffu;  // sources[i] >= 0: a vertex on that triangle (its occluder mask)
+      if (IPT_SHADOW_PO && sources && a.pomask && sources[i] >= 0) {
+        int e = 0;
+        while (e < a.nE - 1 && emit_tri[e] != target) ++e;
+        allow = a.pomask[sources[i] * a.nE + e];
+      }
+      h = shadow_hit_pairs_small((const lds_f32 *)lds_is, pairs, a.pboxes, e3, nT, p, d, target, t, allow);
+    }
     else if (!BVH && IPT_PATH_CULL && small && targets && target < 0)  // ... and its path cast
       h = closest_hit_pairs_culled((const lds_f32 *)lds_pr, a.pboxes, nT, p, d, t);
     else
@@ -2346,7 +2369,7 @@ int gpu_set_accel(GpuScene *s, int mode) {
 int gpu_accel_in_use(const GpuScene *s) { return use_bvh(s) ? IPT_ACCEL_BVH : IPT_ACCEL_BRUTE; }
 
 int gpu_closest_hit(GpuScene *s, int64_t n, const float *org_dev, const float *dir_dev, const int *targets_dev,
-                    float *t_dev, int *idx_dev, void *stream) {
+                    const int *sources_dev, float *t_dev, int *idx_dev, void *stream) {
   if (!s->on_device) {
     gpu_set_error("scene was loaded host-only (ipt_load_scene_host); it cannot be traced");
     return -1;
@@ -2359,13 +2382,15 @@ int gpu_closest_hit(GpuScene *s, int64_t n, const float *org_dev, const float *d
   if (use_bvh(s)) {
     const size_t lds = bvh_lds(s, a, base, false);
     hipLaunchKernelGGL(closest_hit_kernel<true>, dim3(blocks), dim3(kBlock), lds, (hipStream_t)stream, s->isect,
-                       s->pairs, s->bnodes, s->bpairs, a, small, n, org_dev, dir_dev, targets_dev, t_dev, idx_dev);
+                       s->pairs, s->bnodes, s->bpairs, a, small, n, org_dev, dir_dev, targets_dev, sources_dev,
+                       s->emit_tri, t_dev, idx_dev);
   } else {
     const size_t lds = base + (small ? 12 + (size_t)s->host.nT * sizeof(TriIsect) +
                                            (IPT_PATH_CULL ? (size_t)((s->host.nT + 1) / 2) * sizeof(TriPair) : 0)
                                      : 0);
     hipLaunchKernelGGL(closest_hit_kernel<false>, dim3(blocks), dim3(kBlock), lds, (hipStream_t)stream, s->isect,
-                       s->pairs, s->bnodes, s->bpairs, a, small, n, org_dev, dir_dev, targets_dev, t_dev, idx_dev);
+                       s->pairs, s->bnodes, s->bpairs, a, small, n, org_dev, dir_dev, targets_dev, sources_dev,
+                       s->emit_tri, t_dev, idx_dev);
   }
   HIP_TRY(hipGetLastError());
   return 0;
@@ -2416,10 +2441,10 @@ int gpu_adjoint_host(GpuScene *s, const RenderParams &p, const float *adj, doubl
   return 0;
 }
 
-int gpu_closest_hit_host(GpuScene *s, int64_t n, const float *org, const float *dir, const int *targets, float *t,
-                         int *idx) {
+int gpu_closest_hit_host(GpuScene *s, int64_t n, const float *org, const float *dir, const int *targets,
+                         const int *sources, float *t, int *idx) {
   if (n <= 0) return 0;
-  DevBuf o, d, g, tt, ii;
+  DevBuf o, d, g, sr, tt, ii;
   const size_t n3 = (size_t)n * 3 * sizeof(float);
   HIP_TRY(hipMalloc(&o.p, n3));
   HIP_TRY(hipMalloc(&d.p, n3));
@@ -2431,8 +2456,12 @@ int gpu_closest_hit_host(GpuScene *s, int64_t n, const float *org, const float *
     HIP_TRY(hipMalloc(&g.p, (size_t)n * sizeof(int)));
     HIP_TRY(hipMemcpy(g.p, targets, (size_t)n * sizeof(int), hipMemcpyHostToDevice));
   }
-  if (gpu_closest_hit(s, n, (const float *)o.p, (const float *)d.p, (const int *)g.p, (float *)tt.p, (int *)ii.p,
-                      nullptr))
+  if (sources) {
+    HIP_TRY(hipMalloc(&sr.p, (size_t)n * sizeof(int)));
+    HIP_TRY(hipMemcpy(sr.p, sources, (size_t)n * sizeof(int), hipMemcpyHostToDevice));
+  }
+  if (gpu_closest_hit(s, n, (const float *)o.p, (const float *)d.p, (const int *)g.p, (const int *)sr.p,
+                      (float *)tt.p, (int *)ii.p, nullptr))
     return -1;
   HIP_TRY(hipMemcpy(t, tt.p, (size_t)n * sizeof(float), hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(idx, ii.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));

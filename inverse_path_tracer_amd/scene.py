@@ -211,6 +211,28 @@ class Scene:
                                              t.ctypes.data_as(N.fp), idx.ctypes.data_as(ip)), "closest_hit")
         return t, idx
 
+    def shadow_masks(self):
+        """uint32[nT, max(nE, 1)]: the shadow rays' potential-occluder pair masks."""
+        m = np.zeros((self.nT, max(1, self.nE)), np.uint32)
+        N.check(N.lib().ipt_scene_shadow_masks(self.handle, m.ctypes.data_as(C.POINTER(C.c_uint32))), "shadow_masks")
+        return m
+
+    def shadow_hit(self, origins, dirs, targets, sources):
+        """Shadow rays as the megakernel casts them from a vertex on triangle
+        sources[i] (< 0: unknown) towards emitter triangle targets[i]."""
+        o = np.ascontiguousarray(np.asarray(origins, np.float32).reshape(-1, 3))
+        d = np.ascontiguousarray(np.asarray(dirs, np.float32).reshape(-1, 3))
+        n = o.shape[0]
+        t = np.zeros(n, np.float32)
+        idx = np.zeros(n, np.int32)
+        tg = np.ascontiguousarray(np.asarray(targets, np.int32).reshape(n))
+        sr = np.ascontiguousarray(np.asarray(sources, np.int32).reshape(n))
+        ip = C.POINTER(C.c_int32)
+        N.check(N.lib().ipt_shadow_hit_host(self.handle, n, o.ctypes.data_as(N.fp), d.ctypes.data_as(N.fp),
+                                            tg.ctypes.data_as(ip), sr.ctypes.data_as(ip), t.ctypes.data_as(N.fp),
+                                            idx.ctypes.data_as(ip)), "shadow_hit")
+        return t, idx
+
     # ---------------------------------------------------------- host-memory renders
     def render_samples(self, width, height, spp, max_bounces=None, seed=0, row_begin=0, row_end=None, row_step=1):
         p = N.make_params(width, height, spp, max_bounces, seed, row_begin, row_end, row_step)

@@ -302,3 +302,53 @@ def test_quantised_wide_nodes_contain_exact_boxes(name):
     assert np.all(ql[~used][:, 0] > qh[~used][:, 0])
     # tight: each bound within one grid step of the exact one
     assert np.all(exact_lo[used] - lo[used] < np.broadcast_to(step[:, None, :], lo.shape)[used])
+
+
+def _shadow_rays(tris, n, rng, edge_frac=0.3):
+    """Shadow rays as the megakernel builds them: origin on a random source
+    triangle, target point on a random emitter (near its edges and corners
+    for edge_frac of them); returns O, D, targets, sources, emitter index."""
+    emit = np.nonzero(tris[:, 56] >= 0)[0]
+    v = tris[:, 0:9].reshape(-1, 3, 3).astype(np.float64)
+
+    def on_tri(idx, a, b):
+        flip = a + b > 1
+        a, b = np.where(flip, 1 - a, a), np.where(flip, 1 - b, b)
+        return v[idx, 0] + a[:, None] * (v[idx, 1] - v[idx, 0]) + b[:, None] * (v[idx, 2] - v[idx, 0])
+
+    src = rng.randint(0, len(tris), n)
+    O = on_tri(src, *rng.uniform(0, 1, (2, n)))
+    e = rng.randint(0, len(emit), n)
+    ab = rng.uniform(0, 1, (2, n))
+    edge = rng.uniform(0, 1, n) < edge_frac
+    ab[:, edge] = np.round(ab[:, edge] * 4) / 4 + rng.normal(0, 1e-6, (2, int(edge.sum())))
+    pt = on_tri(emit[e], np.clip(ab[0], 0, 1), np.clip(ab[1], 0, 1))
+    D = pt - O
+    dist = np.linalg.norm(D, axis=1)
+    D /= dist[:, None]
+    return O.astype(np.float32), D.astype(np.float32), emit[e].astype(np.int32), src.astype(np.int32), e, dist
+
+
+@pytest.mark.parametrize("which", ["cornell", "scene0"])
+def test_shadow_occluder_masks_are_conservative(oracle, which):
+    """bvh.cpp shadow_occluder_masks: whenever the oracle's closest hit of a
+    shadow ray from a point on triangle s towards emitter e is an occluder
+    (not the target, no farther than the target point), that occluder's pair
+    is in mask[s, e]; the emitter's own
+    pair is always in; and the masks do leave pairs out."""
+    recs = CORNELL if which == "cornell" else SCENE0
+    P = product_scene(recs, device=False)
+    Q = oracle.OracleScene(recs)
+    tris = P.triangles()
+    m = P.shadow_masks()
+    O, D, tg, src, e, dist = _shadow_rays(tris, 200000, np.random.RandomState(17))
+    t, idx = Q.closest_hit(O, D)
+    occ = (idx >= 0) & (idx != tg) & (t <= dist * (1 + 1e-5))  # a hit beyond: the target itself was missed
+    assert occ.mean() > 0.001
+    bit = np.where(idx >= 0, idx // 2, 0).astype(np.uint32)
+    assert np.all((m[src[occ], e[occ]] >> bit[occ]) & 1)
+    emit = np.nonzero(tris[:, 56] >= 0)[0]
+    for k, et in enumerate(emit):
+        assert np.all((m[:, k] >> (et // 2)) & 1)
+    assert np.all(m < (1 << ((P.nT + 1) // 2)))
+    assert min(bin(int(x)).count("1") for x in m.ravel()) < (P.nT + 1) // 2

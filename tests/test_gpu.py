@@ -602,3 +602,24 @@ def test_culled_path_cast_equals_brute_force(oracle, which):
     hit = iq >= 0
     assert np.array_equal(bits(tq[hit]), bits(tc[:60000][hit]))
     P.close()
+
+
+@pytest.mark.parametrize("which", ["cornell", "scene0"])
+def test_masked_shadow_query_equals_brute_force(which):
+    """The megakernel's shadow cast with the static potential-occluder mask of
+    its (source triangle, emitter) answers "closest hit is the target, at t"
+    exactly as the full brute-force loop: origins on every triangle (shadow
+    rays along the light's own plane included), targets on the emitters near
+    their edges and corners (ties with the coplanar ceiling)."""
+    from test_bvh import _shadow_rays
+
+    P = product_scene(CORNELL if which == "cornell" else SCENE0)
+    O, D, tg, src, _, _ = _shadow_rays(P.triangles(), 400000, np.random.RandomState(23))
+    src[::7] = -1  # no mask for some: the plain culled cast
+    tc, ic = P.shadow_hit(O, D, tg, src)
+    tf, i_f = P.closest_hit(O, D)
+    vis_c, vis_f = ic == tg, i_f == tg
+    assert np.array_equal(vis_c, vis_f)
+    assert 0.05 < vis_f.mean() < 0.98
+    assert np.array_equal(bits(tc[vis_c]), bits(tf[vis_f]))
+    P.close()
