@@ -337,7 +337,13 @@ std::vector<PairBox2> pair_boxes(const HostScene &S) {
 // own pair (coplanar partner) always stays; in a room, a wall on whose plane
 // S ends (a neighbour) is left out thanks to the 1e-2 lower end.
 std::vector<uint32_t> shadow_occluder_masks(const HostScene &S) {
-  const int nT = S.nT, nE = S.nE, nP = (nT + 1) / 2;
+  std::vector<int> tri((size_t)((S.nT + 1) / 2) * 2);
+  for (size_t k = 0; k < tri.size(); ++k) tri[k] = (int)k < S.nT ? (int)k : -1;
+  return shadow_occluder_masks(S, tri);
+}
+
+std::vector<uint32_t> shadow_occluder_masks(const HostScene &S, const std::vector<int> &pair_tris) {
+  const int nT = S.nT, nE = S.nE, nP = (int)pair_tris.size() / 2;
   const uint32_t all = nP >= 32 ? 0xffffffffu : ((1u << nP) - 1u);
   std::vector<uint32_t> out((size_t)nT * (size_t)std::max(nE, 1), all);
   if (nP > 32 || nE == 0) return out;
@@ -391,8 +397,8 @@ std::vector<uint32_t> shadow_occluder_masks(const HostScene &S) {
       for (int j = 0; j < nP; ++j) {
         bool excluded = true;
         for (int hh = 0; hh < 2 && excluded; ++hh) {
-          const int w = 2 * j + hh;
-          if (w >= nT) continue;  // the padding triangle is never accepted
+          const int w = pair_tris[(size_t)(2 * j + hh)];
+          if (w < 0 || w >= nT) continue;  // the padding triangle is never accepted
           const TriIsect &T = S.isect[(size_t)w];
           const double n[3] = {T.n[0], T.n[1], T.n[2]};
           if (n[0] == 0.0 && n[1] == 0.0 && n[2] == 0.0) continue;  // never accepted

@@ -32,5 +32,8 @@ std::vector<PairBox2> pair_boxes(const HostScene &S);
 // Per (source triangle, emitter): the pairs that might occlude a shadow ray
 // (bit j = pair j), nT * nE words; see bvh.cpp.
 std::vector<uint32_t> shadow_occluder_masks(const HostScene &S);
+// The same over an explicit pair list (2 triangle indices per pair; < 0 or
+// >= nT = padding): the BVH scenes' large-triangle pairs.
+std::vector<uint32_t> shadow_occluder_masks(const HostScene &S, const std::vector<int> &pair_tris);
 
 }  // namespace ipt

@@ -607,7 +607,7 @@ constexpr int kBvhDone = (int)0x80000000;
 // triangle tests, [5] coop calls with >= 1 ray (per wave), [6] coop rounds
 // (per wave); pre-pass: [7] casts, [8] large-triangle tests, [9] shadow
 // target tests, [10] shadow rays decided before the tree.
-constexpr int kBvhStats = 21;  // [12..17]: culled shadow casts (shadow_hit_pairs_small); [18..20]: culled path casts
+constexpr int kBvhStats = 23;  // [12..17]: culled shadow casts (shadow_hit_pairs_small); [18..22]: culled path casts
 #ifdef IPT_BVH_STATS
 __device__ unsigned long long g_bvh_stats[kBvhStats];
 #endif
@@ -891,6 +891,17 @@ __device__ __forceinline__ int closest_hit_pairs_culled(const lds_f32 *pairs_lds
   atomicAdd(&g_bvh_stats[18], 1ull);                                            // path casts
   atomicAdd(&g_bvh_stats[19], (unsigned long long)__builtin_popcount(need));    // lane pair tests
   atomicAdd(&g_bvh_stats[20], (unsigned long long)nP);                          // lane box tests
+  {
+    const uint64_t act = __builtin_amdgcn_ballot_w64(true);
+    const bool first = __lane_id() == __ffsll((unsigned long long)act) - 1;
+    uint32_t mx = need;  // wave loop trips = max over lanes of popcount(need)
+    int trips = __builtin_popcount(mx);
+    for (int o = 32; o >= 1; o >>= 1) trips = max(trips, __shfl_xor(trips, o));
+    if (first) {
+      atomicAdd(&g_bvh_stats[21], 1ull);                                        // wave-level calls
+      atomicAdd(&g_bvh_stats[22], (unsigned long long)trips);                   // wave-level loop trips
+    }
+  }
 #endif
   while (need) {  // per lane: the wave loops while any lane has a pair left
     const int j = __builtin_ctz(need);
@@ -951,7 +962,8 @@ __device__ __forceinline__ void bvh_big_pass_culled(const BvhView &B, V3 p, V3 d
 // test (target >= 0) and the large-triangle pre-pass.  Returns false when
 // the cast is already decided (shadow target missed or occluded).
 template <bool SHADOW>
-__device__ __forceinline__ bool bvh_prepass(const BvhView &B, V3 p, V3 d, float &bt, int &bi, int target) {
+__device__ __forceinline__ bool bvh_prepass(const BvhView &B, V3 p, V3 d, float &bt, int &bi, int target,
+                                            uint32_t allow = 0xffffffffu) {
   bt = __builtin_inff();
   bi = -1;
 #ifdef IPT_ABL_NOTARGET  // timing-only ablation build: no target test (wrong shadows)
@@ -987,7 +999,7 @@ __device__ __forceinline__ bool bvh_prepass(const BvhView &B, V3 p, V3 d, float 
     const cst_i32 *bidx = (const cst_i32 *)B.big_idx;
     const PairBox2 *boxes = B.big_boxes;
     asm volatile("" : "+s"(boxes));
-    const uint32_t need = pair_box_bits(boxes, nP, p, d, bt);
+    const uint32_t need = pair_box_bits(boxes, nP, p, d, bt, allow);
     const bool vis = occlusion_pass([&](int j) { return load_pair_cst(B.big + j); }, [&](int k) { return bidx[k]; },
                                     e3l, nP, need, p, d, target, bt, true);
     if (!vis) {  // occluded by a large triangle: decided

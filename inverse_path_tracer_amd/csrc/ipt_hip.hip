@@ -204,6 +204,8 @@ struct TraceArgs {
   // small scenes: potential occluders per (source triangle, emitter), nT*nE
   // words (bvh.cpp shadow_occluder_masks), copied to LDS; nullptr = none
   const uint32_t *pomask;
+  // BVH scenes: the same masks over the large-triangle pairs (nullptr = none)
+  const uint32_t *big_pomask;
 };
 static_assert(alignof(TraceArgs) == 8, "TraceArgs sits right after the ten 8-B scene pointers in the kernarg segment");
 
@@ -1022,7 +1024,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     if (__ballot(shadow)) {
       if (BVH && kCoop) {
         bool qn = false;
-        if (shadow && bvh_prepass<true>(bv, p, sd, ts, hs, et)) qn = coop_root_test(cv, p, sd, ts);
+        if (shadow && bvh_prepass<true>(bv, p, sd, ts, hs, et,
+                                        a.big_pomask ? a.big_pomask[tri * nE + emitter] : 0xffffffffu))
+          qn = coop_root_test(cv, p, sd, ts);
         coop_cast<true>(cv, qn, p, sd, ts, hs);
       } else if (!SERVE && shadow) {
         if (!BVH && IPT_SHADOW_CULL && e3)
@@ -1578,6 +1582,7 @@ struct GpuScene {
   TriIsect *wtris = nullptr;
   PairBox2 *pboxes = nullptr;  // pair acceptance boxes (small scenes' culled shadow casts)
   uint32_t *pomask = nullptr;  // shadow rays' potential occluders (small scenes)
+  uint32_t *big_pomask = nullptr;  // ... over the large-triangle pairs (BVH scenes)
   int accel = IPT_ACCEL_AUTO;
   int *grad_map = nullptr, *slot_tri = nullptr;  // ADJ hot-set LDS slots (large scenes)
   int grid[16] = {0};       // resident workgroups per (mode, spec, bvh) (0 = not queried)
@@ -1639,7 +1644,11 @@ GpuScene *gpu_upload(const HostScene &host, std::string *err) {
       upload(&s->big_boxes, host.bvh_big_boxes) ||
       (IPT_BVH_QNODES ? upload_as_f4(&s->wide, host.bvh_qwide) : upload_as_f4(&s->wide, host.bvh_wide)) ||
       upload(&s->wtris, host.bvh_wtris) || upload(&s->pboxes, pair_boxes(host)) ||
-      upload(&s->pomask, shadow_occluder_masks(host))) {
+      upload(&s->pomask, shadow_occluder_masks(host)) ||
+      upload(&s->big_pomask, host.bvh_big_idx.empty()
+                                 ? std::vector<uint32_t>()
+                                 : shadow_occluder_masks(host, std::vector<int>(host.bvh_big_idx.begin(),
+                                                                                host.bvh_big_idx.end())))) {
     *err = gpu_last_error();
     gpu_free(s);
     return nullptr;
@@ -1704,6 +1713,7 @@ void gpu_free(GpuScene *s) {
   (void)hipFree(s->wtris);
   (void)hipFree(s->pboxes);
   (void)hipFree(s->pomask);
+  (void)hipFree(s->big_pomask);
   (void)hipFree(s->grad_map);
   (void)hipFree(s->slot_tri);
   delete s;
@@ -1825,6 +1835,7 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.chunk_ctr = nullptr;
   a.pboxes = s->pboxes;
   a.pomask = s->host.nE > 0 ? s->pomask : nullptr;
+  a.big_pomask = nullptr;  // set with the other BVH fields (bvh_lds)
   a.nscenes = p.nscenes > 1 ? p.nscenes : 1;
   a.bps = 1;
   a.seed_stride = p.seed_stride;
@@ -1857,6 +1868,7 @@ static size_t bvh_lds(const GpuScene *s, TraceArgs &a, size_t base, bool server,
   a.bvh_wtris = s->wtris;
   a.bvh_wide_lds = (stage && kCoop && nw * kWideF4 * sizeof(float4) <= (size_t)kBvhLdsNodeBytes) ? (int)nw : 0;
   a.bvh_big_lds = big_copy && IPT_PATH_CULL ? 1 : 0;
+  a.big_pomask = (IPT_SHADOW_PO && s->host.nE > 0 && !s->host.bvh_big_idx.empty()) ? s->big_pomask : nullptr;
   a.coop_stride = 7 * s->host.bvh_wdepth + 8;
   a.bvh_stack = std::max(1, s->host.bvh_depth);
   a.bvh_nbig = (int)s->host.bvh_big_pairs.size();
@@ -2325,7 +2337,13 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
     bool qn = false;
     if (valid) {
       if (target >= 0) {
-        if (bvh_prepass<true>(bv, p, d, t, h, target)) qn = coop_root_test(cv, p, d, t);
+        uint32_t allow = 0xffffffffu;  // sources[i] >= 0: a vertex on that triangle (its occluder mask)
+        if (IPT_SHADOW_PO && sources && a.big_pomask && sources[i] >= 0) {
+          int e = 0;
+          while (e < a.nE - 1 && emit_tri[e] != target) ++e;
+          allow = a.big_pomask[sources[i] * a.nE + e];
+        }
+        if (bvh_prepass<true>(bv, p, d, t, h, target, allow)) qn = coop_root_test(cv, p, d, t);
       } else {
         bvh_prepass<false>(bv, p, d, t, h, -1);
         qn = coop_root_test(cv, p, d, t);

@@ -31,7 +31,8 @@ from inverse_path_tracer_amd.scene import ObjectSpec, Scene  # noqa: E402
 NAMES = ["tree_rays", "node_visits", "leaf_visits", "shadow_occluded_in_tree", "leaf_tri_tests", "coop_calls",
          "coop_rounds", "casts", "prepass_tri_tests", "shadow_target_tests", "shadow_decided_before_tree", "unused",
          "cull_shadow_lanes", "cull_target_accepted", "cull_wave_calls", "cull_wave_pair_tests",
-         "cull_lane_pair_tests", "cull_lane_box_tests", "pcull_casts", "pcull_lane_pair_tests", "pcull_lane_box_tests"]
+         "cull_lane_pair_tests", "cull_lane_box_tests", "pcull_casts", "pcull_lane_pair_tests", "pcull_lane_box_tests", "pcull_wave_calls",
+         "pcull_wave_trips"]
 
 
 def derive(c, n):
@@ -57,7 +58,9 @@ def derive(c, n):
             "pcull_casts_per_sample": c.get("pcull_casts", 0) / n,
             "pcull_tri_tests_per_sample": 2 * c.get("pcull_lane_pair_tests", 0) / n,
             "pcull_pairs_per_cast": c.get("pcull_lane_pair_tests", 0) / max(1, c.get("pcull_casts", 0)),
-            "pcull_box_tests_per_sample": c.get("pcull_lane_box_tests", 0) / n}
+            "pcull_box_tests_per_sample": c.get("pcull_lane_box_tests", 0) / n,
+            "pcull_lanes_per_wave_call": c.get("pcull_casts", 0) / max(1, c.get("pcull_wave_calls", 0)),
+            "pcull_trips_per_wave_call": c.get("pcull_wave_trips", 0) / max(1, c.get("pcull_wave_calls", 0))}
 
 
 def main():
