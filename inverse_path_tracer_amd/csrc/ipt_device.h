@@ -742,6 +742,14 @@ __device__ __forceinline__ SlabRay slab_ray(V3 p, V3 d) {
 #ifndef IPT_SHADOW_PO
 #define IPT_SHADOW_PO 1
 #endif
+// IPT_SHADOW_TARGET_PAIR=1: the culled shadow cast tests the target with its
+// pair partner (gathered from the path cull's LDS pair copy), see
+// shadow_hit_pairs_small.  Measured slower (C2 forward 1.68 -> 1.83 ms): the
+// 36 gathered floats, live next to the shading state, spill 44-48 B per lane
+// (profiles/r02_variants_shadow_target_pair.log).  Off.
+#ifndef IPT_SHADOW_TARGET_PAIR
+#define IPT_SHADOW_TARGET_PAIR 0
+#endif
 typedef __attribute__((address_space(3))) const uint32_t lds_u32c;
 // Bit j: the ray enters pair j's acceptance box within [kEpsUp, bt] (the
 // pairs' boxes two per PairBox2 record; scalar loads).
@@ -810,20 +818,49 @@ __device__ __forceinline__ bool occlusion_pass(PairAt pair_at, IdxAt idx_at, lds
   return live;
 }
 
+// A TriPair from an LDS copy (per-lane gather: nine 16-B reads).
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const f4v lds_f4c;
+__device__ __forceinline__ TriPair load_pair_lds(const lds_f32 *pl, int j) {
+  const lds_f4c *q = (const lds_f4c *)(pl + 36 * j);
+  TriPair T;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const f4v v = q[k];
+    T.f[2 * k][0] = v.x;
+    T.f[2 * k][1] = v.y;
+    T.f[2 * k + 1][0] = v.z;
+    T.f[2 * k + 1][1] = v.w;
+  }
+  return T;
+}
+// pairs_lds (the culled path cast's TriPair copy, or nullptr): the target is
+// decided together with its pair partner -- the in-order loop over the
+// target's own pair from the empty state (packed, gathered per lane), which
+// also settles whether the partner occludes or ties ahead of it -- and that
+// pair leaves the occlusion pass.
 __device__ __forceinline__ int shadow_hit_pairs_small(const lds_f32 *isect_lds, const TriPair *__restrict__ pairs,
                                                       const PairBox2 *__restrict__ boxes, const f2 *e3, int nT, V3 p,
-                                                      V3 d, int target, float &best_t, uint32_t allow = 0xffffffffu) {
+                                                      V3 d, int target, float &best_t, uint32_t allow = 0xffffffffu,
+                                                      const lds_f32 *pairs_lds = nullptr) {
   float bt = __builtin_inff();
   int bi = -1;
-  {  // the target's record from the LDS copy of the TriIsect array
+  bool live;
+  if (pairs_lds) {
+    const int jt = target >> 1;
+    const TriPair T = load_pair_lds(pairs_lds, jt);
+    pair_ray(T, pair_origin(T, p), 2 * jt, 2 * jt + 1, p, d, bt, bi, ld2(T, 9), ld2(T, 13), ld2(T, 17));
+    live = bi == target;
+    allow &= ~(1u << jt);
+  } else {  // the target's record from the LDS copy of the TriIsect array
     TriIsect T;
     float *tf = reinterpret_cast<float *>(&T);
     const lds_f32 *q = isect_lds + 20 * target;
 #pragma unroll
     for (int k = 0; k < 20; ++k) tf[k] = q[k];
     hit_test(T, target, p, d, bt, bi);
+    live = bi >= 0;
   }
-  bool live = bi >= 0;
   int nP = (nT + 1) >> 1;
   asm volatile("" : "+s"(nP));
   lds_f2c *e3l = (lds_f2c *)e3;
@@ -845,6 +882,7 @@ __device__ __forceinline__ int shadow_hit_pairs_small(const lds_f32 *isect_lds, 
                           live);
     if (!live && bi >= 0) bi = -1;  // occluded: not the target (the caller only compares with it)
   }
+  if (!live) bi = -1;
   best_t = bt;
   return bi;
 }
@@ -864,21 +902,6 @@ __device__ __forceinline__ int shadow_hit_pairs_small(const lds_f32 *isect_lds, 
 #ifndef IPT_PATH_CULL
 #define IPT_PATH_CULL 1
 #endif
-typedef float f4v __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) const f4v lds_f4c;
-__device__ __forceinline__ TriPair load_pair_lds(const lds_f32 *pl, int j) {
-  const lds_f4c *q = (const lds_f4c *)(pl + 36 * j);
-  TriPair T;
-#pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    const f4v v = q[k];
-    T.f[2 * k][0] = v.x;
-    T.f[2 * k][1] = v.y;
-    T.f[2 * k + 1][0] = v.z;
-    T.f[2 * k + 1][1] = v.w;
-  }
-  return T;
-}
 __device__ __forceinline__ int closest_hit_pairs_culled(const lds_f32 *pairs_lds, const PairBox2 *__restrict__ boxes,
                                                         int nT, V3 p, V3 d, float &best_t) {
   float bt = __builtin_inff();

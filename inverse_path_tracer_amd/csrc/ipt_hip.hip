@@ -1031,7 +1031,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       } else if (!SERVE && shadow) {
         if (!BVH && IPT_SHADOW_CULL && e3)
           hs = shadow_hit_pairs_small((const lds_f32 *)lds_is, pairs, a.pboxes, e3, nT, p, sd, et, ts,
-                                      po ? ((const lds_u32c *)lds_po)[tri * nE + emitter] : 0xffffffffu);
+                                      po ? ((const lds_u32c *)lds_po)[tri * nE + emitter] : 0xffffffffu,
+                                      IPT_PATH_CULL && IPT_SHADOW_TARGET_PAIR ? (const lds_f32 *)lds_pr : nullptr);
         else
           hs = cast<BVH>(isect, pairs, e3, nT, bv, p, sd, ts, et);
       }
@@ -2359,7 +2360,8 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
         while (e < a.nE - 1 && emit_tri[e] != target) ++e;
         allow = a.pomask[sources[i] * a.nE + e];
       }
-      h = shadow_hit_pairs_small((const lds_f32 *)lds_is, pairs, a.pboxes, e3, nT, p, d, target, t, allow);
+      h = shadow_hit_pairs_small((const lds_f32 *)lds_is, pairs, a.pboxes, e3, nT, p, d, target, t, allow,
+                                 IPT_PATH_CULL && IPT_SHADOW_TARGET_PAIR ? (const lds_f32 *)lds_pr : nullptr);
     }
     else if (!BVH && IPT_PATH_CULL && small && targets && target < 0)  // ... and its path cast
       h = closest_hit_pairs_culled((const lds_f32 *)lds_pr, a.pboxes, nT, p, d, t);
