@@ -877,7 +877,10 @@ __device__ __forceinline__ int shadow_hit_pairs_small(const lds_f32 *isect_lds, 
   asm volatile("" : "+s"(boxes));
   if (__builtin_amdgcn_ballot_w64(live)) {
     // box bits first, so that the slab registers are dead before the pair tests
-    const uint32_t need = pair_box_bits(boxes, nP, p, d, bt, live ? allow : 0u);
+    // the target's own pair is always needed (the ray ends in its box and the
+    // partner may tie ahead of the target): its bit is set without a box test
+    const uint32_t tbit = 1u << (target >> 1);
+    const uint32_t need = live ? (pair_box_bits(boxes, nP, p, d, bt, allow & ~tbit) | tbit) : 0u;
     live = occlusion_pass([&](int j) { return pairs[j]; }, [&](int k) { return k; }, e3l, nP, need, p, d, target, bt,
                           live);
     if (!live && bi >= 0) bi = -1;  // occluded: not the target (the caller only compares with it)
