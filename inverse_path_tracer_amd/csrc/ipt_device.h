@@ -1417,8 +1417,11 @@ __device__ __forceinline__ V3 shading_normal(const TriGeom &g, V3 q) {
 // Camera ray (path_trace.cu:155-165) + Ray::transform (scene_basics.h:307-319)
 // rcW / rcH: 1/W and 1/H when W and H are powers of two (then x * rcW == x / W
 // exactly: a power-of-two scale of a normal float), else 0 (divide).
-__device__ __forceinline__ void camera_ray(const float *cam, Rng &st, int r, int c, int W, int H, float rcW,
-                                           float rcH, V3 &p, V3 &d) {
+// org: the camera origin M * (0,0,0,1) = fma(M3, 1, fma(M2, 0, fma(M1, 0, M0 * 0)))
+// per row, the same for every ray: evaluated once on the host with these
+// operations (the launch arguments' cam_org) instead of per lane.
+__device__ __forceinline__ void camera_ray(const float *cam, const float *org, Rng &st, int r, int c, int W, int H,
+                                           float rcW, float rcH, V3 &p, V3 &d) {
   const float u0 = uniform(st), u1 = uniform(st);
   // (2(c+u0)) / W: numerator in [2^-32, 2W], W >= 1 -- in div_inrange's range.
   // d0 = (x, y, 1): x and y are 0 or multiples of 2^-24 (Sterbenz), n2 in
@@ -1427,14 +1430,13 @@ __device__ __forceinline__ void camera_ray(const float *cam, Rng &st, int r, int
   const float x = (rcW != 0.f ? nx * rcW : div_inrange(nx, (float)W)) - 1.f;
   const float y = 1.f - (rcH != 0.f ? ny * rcH : div_inrange(ny, (float)H));
   const V3 d0 = unit_in_range(mk(x, y, 1.f));
-  float pr[3], dr[3];
+  float dr[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const float *M = cam + 4 * i;
-    pr[i] = fmaf(M[3], 1.f, fmaf(M[2], 0.f, fmaf(M[1], 0.f, M[0] * 0.f)));
     dr[i] = fmaf(M[3], 0.f, fmaf(M[2], d0.z, fmaf(M[1], d0.y, M[0] * d0.x)));
   }
-  p = mk(pr[0], pr[1], pr[2]);
+  p = mk(org[0], org[1], org[2]);
   d = unit(mk(dr[0], dr[1], dr[2]));
 }
 

@@ -177,6 +177,7 @@ struct TraceArgs {
   const int *grad_map;
   const int *slot_tri;
   float cam[16];
+  float cam_org[3];  // the camera origin M * (0,0,0,1) with camera_ray's own operations (host, same IEEE ops)
   // 1/spp when spp is a power of two (then x * rc_spp == x / spp for every
   // float x: both are the correctly rounded x * 2^-k), else 0
   float rc_spp;
@@ -278,7 +279,7 @@ __device__ __forceinline__ void item_ray(const TraceArgs &a, uint64_t seed, uint
     g = ((uint64_t)r * (uint64_t)a.W + (uint64_t)c) * (uint64_t)a.spp + sj;
   }
   rng_init(st, seed + g);
-  camera_ray(a.cam, st, r, c, a.W, a.H, a.rc_W, a.rc_H, p, d);
+  camera_ray(a.cam, a.cam_org, st, r, c, a.W, a.H, a.rc_W, a.rc_H, p, d);
 }
 
 // ---------------------------------------------------------------------------
@@ -1830,6 +1831,10 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.grad_map = nullptr;
   a.slot_tri = nullptr;
   std::memcpy(a.cam, s->host.cam, sizeof a.cam);
+  for (int i = 0; i < 3; ++i) {  // camera_ray's pr[i], evaluated once: fmaf is the IEEE fma on host and device
+    const float *M = a.cam + 4 * i;
+    a.cam_org[i] = std::fmaf(M[3], 1.f, std::fmaf(M[2], 0.f, std::fmaf(M[1], 0.f, M[0] * 0.f)));
+  }
   a.use_ring = 0;
   a.rec_cap = p.max_bounces >= 0 ? p.max_bounces + 1 : 0;
   a.chunk = 0;
