@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -177,7 +178,10 @@ struct TraceArgs {
   const int *grad_map;
   const int *slot_tri;
   float cam[16];
-  float cam_org[3];  // the camera origin M * (0,0,0,1) with camera_ray's own operations (host, same IEEE ops)
+  float cam_org[3];
+  // per emitter: 1/pmf when pmf is a power of two (then x * (1/pmf) == x / pmf
+  // exactly), else 0 -- the emitter term's double division becomes a multiply
+  const double *emit_pmfr;  // the camera origin M * (0,0,0,1) with camera_ray's own operations (host, same IEEE ops)
   // 1/spp when spp is a power of two (then x * rc_spp == x / spp for every
   // float x: both are the correctly rounded x * 2^-k), else 0
   float rc_spp;
@@ -1045,7 +1049,13 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           const double td = (double)ts;
           const TriMat &me = mat[et];
           if (MODE == MODE_GRAPH) {
-            const float w2 = (float)(((double)((weight * ct) * ctp) / (td * td)) / (double)emit_pmf[emitter]);
+            const double q = (double)((weight * ct) * ctp) / (td * td), pr = a.emit_pmfr[emitter];
+            double w2d;
+            if (pr != 0.0)
+              w2d = q * pr;
+            else
+              w2d = q / (double)emit_pmf[emitter];
+            const float w2 = (float)w2d;
             const float wf = w2 * kInvPiF;  // BSDF(direct) factor 1/pi, inv_path_trace.cu:8
             const double v[8] = {(double)w2, (double)wf, (double)(wf * pix.x), (double)(wf * pix.y),
                                  (double)(wf * pix.z), (double)(wf * me.ke[0]), (double)(wf * me.ke[1]),
@@ -1061,7 +1071,13 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
 #ifdef IPT_ABL_DP
             const float s = ((ct * ctp) / (ts * ts)) / emit_pmf[emitter];
 #else
-            const float s = (float)(((double)(ct * ctp) / (td * td)) / (double)emit_pmf[emitter]);
+            const double q = (double)(ct * ctp) / (td * td), pr = a.emit_pmfr[emitter];
+            double s64;
+            if (pr != 0.0)
+              s64 = q * pr;
+            else
+              s64 = q / (double)emit_pmf[emitter];
+            const float s = (float)s64;
 #endif
             lo = mk(me.ke[0] * s, me.ke[1] * s, me.ke[2] * s);
             emit_s = s;
@@ -1563,6 +1579,17 @@ __global__ __launch_bounds__(kBlock) void pixel_mean_kernel(const float *__restr
 }
 
 // ---------------------------------------------------------------------------
+// TraceArgs::emit_pmfr: 1/pmf for the power-of-two pmfs (exact multiply), else 0.
+static std::vector<double> pmf_reciprocals(const std::vector<float> &pmf) {
+  std::vector<double> r(pmf.size(), 0.0);
+  for (size_t e = 0; e < pmf.size(); ++e) {
+    int ex = 0;
+    const double m = std::frexp((double)pmf[e], &ex);
+    if (pmf[e] > 0.f && m == 0.5 && ex > -1000) r[e] = std::ldexp(1.0, 1 - ex);
+  }
+  return r;
+}
+
 struct GpuScene {
   HostScene host;
   int device = 0;
@@ -1574,6 +1601,7 @@ struct GpuScene {
   float *kd = nullptr;
   int *emit_tri = nullptr;
   float *emit_cdf = nullptr, *emit_pmf = nullptr;
+  double *emit_pmfr = nullptr;  // TraceArgs::emit_pmfr
   bool has_ks = false;      // some material has a Phong lobe
   BvhNode *bnodes = nullptr;
   BvhPair *bpairs = nullptr;
@@ -1641,7 +1669,7 @@ GpuScene *gpu_upload(const HostScene &host, std::string *err) {
   pack_pairs(host.isect.data(), (int)host.isect.size(), pairs.data());
   if (upload(&s->isect, host.isect) || upload(&s->pairs, pairs) || upload(&s->geom, host.geom) || upload(&s->mat, host.mat) ||
       upload(&s->kd, host.kd) || upload(&s->emit_tri, host.emit_tri) || upload(&s->emit_cdf, host.emit_cdf) ||
-      upload(&s->emit_pmf, host.emit_pmf) || upload(&s->bnodes, host.bvh_nodes) || upload(&s->bpairs, host.bvh_pairs) ||
+      upload(&s->emit_pmf, host.emit_pmf) || upload(&s->emit_pmfr, pmf_reciprocals(host.emit_pmf)) || upload(&s->bnodes, host.bvh_nodes) || upload(&s->bpairs, host.bvh_pairs) ||
       upload(&s->big_pairs, host.bvh_big_pairs) || upload(&s->big_idx, host.bvh_big_idx) ||
       upload(&s->big_boxes, host.bvh_big_boxes) ||
       (IPT_BVH_QNODES ? upload_as_f4(&s->wide, host.bvh_qwide) : upload_as_f4(&s->wide, host.bvh_wide)) ||
@@ -1706,6 +1734,7 @@ void gpu_free(GpuScene *s) {
   (void)hipFree(s->emit_tri);
   (void)hipFree(s->emit_cdf);
   (void)hipFree(s->emit_pmf);
+  (void)hipFree(s->emit_pmfr);
   (void)hipFree(s->bnodes);
   (void)hipFree(s->bpairs);
   (void)hipFree(s->big_pairs);
@@ -1831,6 +1860,7 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.grad_map = nullptr;
   a.slot_tri = nullptr;
   std::memcpy(a.cam, s->host.cam, sizeof a.cam);
+  a.emit_pmfr = s->emit_pmfr;
   for (int i = 0; i < 3; ++i) {  // camera_ray's pr[i], evaluated once: fmaf is the IEEE fma on host and device
     const float *M = a.cam + 4 * i;
     a.cam_org[i] = std::fmaf(M[3], 1.f, std::fmaf(M[2], 0.f, std::fmaf(M[1], 0.f, M[0] * 0.f)));
