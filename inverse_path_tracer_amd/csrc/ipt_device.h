@@ -597,6 +597,7 @@ struct BvhView {
   int nbig;                 // pairs (<= kSmallPairs)
   const PairBox2 *big_boxes;  // the pairs' acceptance boxes (culled shadow pre-pass)
   const float *big_lds;       // LDS copy of the pairs + their indices (culled path pre-pass), or nullptr
+  const float *emit_is;       // LDS copy of the emitters' TriIsect records (shadow target test), or nullptr
 };
 constexpr int kStackStride = 256;  // = the megakernel's block size
 constexpr int kBvhDone = (int)0x80000000;
@@ -988,8 +989,9 @@ __device__ __forceinline__ void bvh_big_pass_culled(const BvhView &B, V3 p, V3 d
 // test (target >= 0) and the large-triangle pre-pass.  Returns false when
 // the cast is already decided (shadow target missed or occluded).
 template <bool SHADOW>
+// eidx: the target's emitter index (its record in B.emit_is), < 0 = unknown.
 __device__ __forceinline__ bool bvh_prepass(const BvhView &B, V3 p, V3 d, float &bt, int &bi, int target,
-                                            uint32_t allow = 0xffffffffu) {
+                                            uint32_t allow = 0xffffffffu, int eidx = -1) {
   bt = __builtin_inff();
   bi = -1;
 #ifdef IPT_ABL_NOTARGET  // timing-only ablation build: no target test (wrong shadows)
@@ -1006,7 +1008,16 @@ __device__ __forceinline__ bool bvh_prepass(const BvhView &B, V3 p, V3 d, float 
   if (SHADOW) atomicAdd(&g_bvh_stats[9], 1ull);
 #endif
   if (SHADOW) {
-    hit_test(B.isect[target], target, p, d, bt, bi);
+    if (B.emit_is && eidx >= 0) {  // from the LDS copy (per-lane gather) instead of L2
+      TriIsect T;
+      float *tf = reinterpret_cast<float *>(&T);
+      const lds_f32 *q = (const lds_f32 *)B.emit_is + 20 * eidx;
+#pragma unroll
+      for (int k = 0; k < 20; ++k) tf[k] = q[k];
+      hit_test(T, target, p, d, bt, bi);
+    } else {
+      hit_test(B.isect[target], target, p, d, bt, bi);
+    }
     if (bi < 0) {  // the target itself is missed: not the closest hit either
 #ifdef IPT_BVH_STATS
       atomicAdd(&g_bvh_stats[10], 1ull);

@@ -501,6 +501,11 @@ __device__ __forceinline__ float small_table_entry(const TriPair *__restrict__ p
 __host__ __device__ inline size_t bvh_lds_offset(size_t base) { return (base + 15) & ~(size_t)15; }
 // Bytes of the culled path pre-pass's LDS copy of the large pairs (16-B
 // aligned, 36 floats per pair) and their original indices (2 ints per pair).
+// The emitters' TriIsect records for the BVH shadow target test (nE <= 16).
+constexpr int kEmitLdsMax = 16;
+__host__ __device__ inline size_t emit_lds_bytes(int nE) {
+  return nE > 0 && nE <= kEmitLdsMax ? (size_t)nE * sizeof(TriIsect) : 0;
+}
 __host__ __device__ inline size_t big_lds_bytes(int nbig) {
   return IPT_PATH_CULL && nbig > 0 ? 12 + (size_t)nbig * (sizeof(TriPair) + 2 * sizeof(int32_t)) : 0;
 }
@@ -630,6 +635,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   bv.nbig = 0;
   bv.big_boxes = nullptr;
   bv.big_lds = nullptr;
+  bv.emit_is = nullptr;
   CoopView cv;
   cv.wn = nullptr;
   cv.wn_lds = false;
@@ -667,6 +673,11 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     bv.big_e3 = reinterpret_cast<const f2 *>(be3);
     bv.nbig = a.bvh_nbig;
     float *after = big_lds_copy(a, be3 + 6 * a.bvh_nbig, reinterpret_cast<float *>(lds), tid, nthr, bv);
+    if (emit_lds_bytes(nE)) {
+      for (int i = tid; i < 20 * nE; i += nthr) after[i] = reinterpret_cast<const float *>(isect)[20 * emit_tri[i / 20] + i % 20];
+      bv.emit_is = after;
+      after += 20 * nE;
+    }
     if (SERVE) {
       srvq = after;
       srvc = reinterpret_cast<int *>(srvq + kQFields * kQSlots);
@@ -1030,7 +1041,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       if (BVH && kCoop) {
         bool qn = false;
         if (shadow && bvh_prepass<true>(bv, p, sd, ts, hs, et,
-                                        a.big_pomask ? a.big_pomask[tri * nE + emitter] : 0xffffffffu))
+                                        a.big_pomask ? a.big_pomask[tri * nE + emitter] : 0xffffffffu, emitter))
           qn = coop_root_test(cv, p, sd, ts);
         coop_cast<true>(cv, qn, p, sd, ts, hs);
       } else if (!SERVE && shadow) {
@@ -1913,7 +1924,7 @@ static size_t bvh_lds(const GpuScene *s, TraceArgs &a, size_t base, bool server,
   a.bvh_big_boxes = s->big_boxes;
   const size_t head = bvh_lds_offset(base) + (size_t)a.bvh_lds_nodes * sizeof(BvhNode) +
                       (size_t)a.bvh_wide_lds * kWideF4 * sizeof(float4) + (size_t)a.bvh_nbig * 6 * sizeof(float) +
-                      (a.bvh_big_lds ? big_lds_bytes(a.bvh_nbig) : 0);
+                      (a.bvh_big_lds ? big_lds_bytes(a.bvh_nbig) : 0) + emit_lds_bytes(s->host.nE);
   if (kCoop) return head + (size_t)(kBlock / 64) * 8 * a.coop_stride * sizeof(uint32_t);
   if (server)
     return head + (size_t)kQFields * kQSlots * sizeof(float) + 8 * sizeof(int) + (size_t)a.bvh_stack * 64 * sizeof(uint32_t);
@@ -2321,6 +2332,7 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
   bv.nbig = 0;
   bv.big_boxes = nullptr;
   bv.big_lds = nullptr;
+  bv.emit_is = nullptr;
   CoopView cv;
   cv.wn = a.bvh_wide;
   cv.wn_lds = false;
