@@ -1,0 +1,88 @@
+#!/bin/bash
+# One GPU-box session (gpurun): tools/gpu.sh TAG STAGE [STAGE ...]
+#
+# Every stage that touches the GPU runs under its own time limit and the
+# stages are chained: the first failure ends the call (no retries).  Outputs
+# go to gpurun_out/<stage>_<TAG>.*; copy what is to be judged into profiles/.
+#
+# Stages:
+#   smoke        __graft_entry__.smoke()
+#   tests        pytest -m gpu ($TESTS, default tests; $PYTEST_K for -k)
+#   bench        bench.py (full JSON line)
+#   benchq       bench.py --no-secondary --no-cpu-baseline
+#   prof         rocprofv3 --kernel-trace --stats of the C2 headline (no secondary lines)
+#   pmc          FETCH_SIZE / WRITE_SIZE passes of the C2 headline (separate runs)
+#   sq           SQ counter passes of the C2 headline
+#   nsprof       rocprofv3 --kernel-trace --stats of the north-star scene (BVH instances)
+#   nspmc        FETCH/WRITE + SQ counter passes of the north-star scene
+#   scenes       tools/bench_scenes.py ($SCENES, default all)
+#   c5           tools/bench_c5.py
+#   graph        tools/bench_graph.py (createGraph at the reference config)
+#   variants     tools/variant_bench.py $VARIANTS ($VB_ONLY scenes; IPT_VB_* passed through)
+#   phase        tools/phase_timing.py
+#   stats        tools/bvh_stats.py with the IPT_BVH_STATS variant library ($SCENES)
+#   multirank    2-rank gloo rehearsal of bench.py on the one GPU
+#   workflow     tools/workflow_at_size.py (pipeline all --n 100 + optimize --n 100)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+R=$(pwd)
+OUT=$R/gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+T=${1:?usage: tools/gpu.sh TAG STAGE...}
+shift
+
+pmc_passes() {  # pmc_passes NAME CMD... : one rocprofv3 run per counter set in $SETS (newline-separated)
+  local name=$1; shift
+  local i=0
+  while IFS= read -r set; do
+    [ -z "$set" ] && continue
+    i=$((i + 1))
+    timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $set -d "$OUT/${name}_${T}_$i" -o run --output-format csv \
+        -- "$@" > "$OUT/${name}_${T}_$i.log" 2>&1 || return 1
+  done <<< "$SETS"
+}
+SQ_SETS="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVES SQ_INSTS_LDS
+SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES
+SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE
+VALUBusy
+VALUUtilization"
+BENCHQ=(python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-secondary)
+NS=(python3 "$R/tools/bench_scenes.py" --scenes northstar --brute-max-tris 0)
+
+run() {
+  case "$1" in
+    smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke_$T.log" 2>&1 ;;
+    tests) timeout -k 10 1000 python -u -m pytest ${TESTS:-tests} -m gpu -v --maxfail=5 --timeout 300 \
+               --timeout-method thread -p no:cacheprovider ${PYTEST_K:+-k "$PYTEST_K"} > "$OUT/pytest_gpu_$T.log" 2>&1 ;;
+    bench) timeout -k 10 600 python bench.py > "$OUT/bench_$T.json" 2> "$OUT/bench_$T.err" ;;
+    benchq) timeout -k 10 300 python bench.py --no-secondary --no-cpu-baseline > "$OUT/benchq_$T.json" 2> "$OUT/benchq_$T.err" ;;
+    prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$T" -o run --output-format csv \
+              -- python3 "$R/bench.py" --steps 20 --warmup 2 --no-cpu-baseline --no-secondary > "$OUT/prof_$T.log" 2>&1 ;;
+    pmc) SETS=$'FETCH_SIZE\nWRITE_SIZE' pmc_passes pmc "${BENCHQ[@]}" ;;
+    sq) SETS=$SQ_SETS pmc_passes sq "${BENCHQ[@]}" ;;
+    nsprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/nsprof_$T" -o run --output-format csv \
+                -- "${NS[@]}" --steps 10 > "$OUT/nsprof_$T.log" 2>&1 ;;
+    nspmc) SETS=$'FETCH_SIZE\nWRITE_SIZE\n'"$SQ_SETS" pmc_passes nspmc "${NS[@]}" --steps 2 ;;
+    scenes) timeout -k 10 300 python tools/bench_scenes.py ${SCENES:+--scenes $SCENES} > "$OUT/scenes_$T.jsonl" 2> "$OUT/scenes_$T.err" ;;
+    c5) timeout -k 10 300 python tools/bench_c5.py > "$OUT/c5_$T.json" 2> "$OUT/c5_$T.err" ;;
+    graph) timeout -k 10 300 python tools/bench_graph.py > "$OUT/graph_$T.json" 2> "$OUT/graph_$T.err" ;;
+    variants) IPT_VB_ONLY=${VB_ONLY:-$IPT_VB_ONLY} timeout -k 10 600 python tools/variant_bench.py ${VARIANTS:-base} \
+                  > "$OUT/variants_$T.log" 2>&1 ;;
+    phase) timeout -k 10 300 python tools/phase_timing.py > "$OUT/phase_$T.log" 2>&1 ;;
+    stats) IPT_AMD_LIB=$R/inverse_path_tracer_amd/lib/variants/libipt_stats.so timeout -k 10 300 \
+               python tools/bvh_stats.py ${SCENES:+--scenes $SCENES} --out "$OUT/stats_$T.json" > "$OUT/stats_$T.log" 2>&1 ;;
+    multirank) IPT_BENCH_DEVICE=0 IPT_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 \
+                   --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 40 \
+                   --warmup 4 > "$OUT/bench_2rank_$T.json" 2> "$OUT/bench_2rank_$T.err" ;;
+    workflow) timeout -k 10 1000 python -u tools/workflow_at_size.py --out "$OUT/workflow_$T.json" > "$OUT/workflow_$T.log" 2>&1 ;;
+    *) echo "unknown stage $1" >&2; return 2 ;;
+  esac
+}
+
+rc=0
+for s in "$@"; do
+  run "$s" || { rc=$?; echo "stage $s failed rc=$rc" > "$OUT/status_$T"; break; }
+done
+[ $rc -eq 0 ] && echo "ok: $*" > "$OUT/status_$T"
+exit $rc
