@@ -70,6 +70,10 @@ PMC_FILE = os.path.join(ROOT, "profiles", "pmc_fwd_trace_kernel.json")
 # (tools/bvh_stats.py -> profiles/bvh_stats.json: 38 per triangle test + 12
 # per slab test)
 CASTS_PER_SAMPLE_C3 = 5.61259913444519
+# createGraph's integrator at the reference's configuration (scenes/0.txt,
+# 500x500, 100 spp, no bounce cap): tools/count_casts.py with the oracle
+CASTS_PER_SAMPLE_GRAPH = 7.1221316
+GRAPH_TARGET = os.path.join(ROOT, "tests", "golden", "preds_0_true.png")  # the reference's preds/0_true.png
 BVH_STATS_FILE = os.path.join(ROOT, "profiles", "bvh_stats.json")
 
 
@@ -133,7 +137,9 @@ def cpu_baseline(seconds_per_leg=1.5):
     recs = {"cornell": [(o.pos, o.ori, o.scl, o.obj_file, o.mtl_file) for o in CORNELL],
             "scene0": [(o.pos, o.ori, o.scl, o.obj_file, o.mtl_file) for o in SCENE0]}
     legs = {"c1_fwd": ("cornell", 128, 128, 8, 2, "fwd"), "c2_fwd": ("cornell", W, H, SPP, BOUNCES, "fwd"),
-            "c3_adj": ("scene0", W, H, SPP, BOUNCES, "adj")}
+            "c3_adj": ("scene0", W, H, SPP, BOUNCES, "adj"), "graph": ("scene0", 500, 500, 100, None, "graph")}
+    from inverse_path_tracer_amd import png_read
+    target = png_read(GRAPH_TARGET)
     out = {}
     for fast in (False, True):
         scenes = {k: oracle_lib.OracleScene(v, fast=fast) for k, v in recs.items()}
@@ -149,6 +155,8 @@ def cpu_baseline(seconds_per_leg=1.5):
                     t0 = time.perf_counter()
                     if kind == "fwd":
                         sc.render_samples(w, h, spp, mb, 0, row * w * spp, (row + r) * w * spp)
+                    elif kind == "graph":
+                        sc.graph(w, h, spp, mb, 0, target, row, row + r)
                     else:
                         sc.adjoint(w, h, spp, mb, 0, adj, row, row + r)
                     secs += time.perf_counter() - t0
@@ -164,6 +172,7 @@ def cpu_baseline(seconds_per_leg=1.5):
                       "C2 frame (%.1f s); legs: C1/C2 forward and C3 adjoint, parity and fast builds, %d cores and "
                       "1 core, >= %.1f s each (table in `legs`)" % (c2["rows"], c2["s"], cores, seconds_per_leg),
             "grad_value": out["c3_adj_fast_all"]["Msamples_s"], "value_1core": out["c2_fwd_fast_1core"]["Msamples_s"],
+            "graph_value": out["graph_fast_all"]["Msamples_s"],
             "cores_note": "%d = this job's CPU share (OMP_NUM_THREADS on the GPU box; %d CPUs in the affinity mask, "
                           "%d in the machine)" % (cores, affinity, os.cpu_count() or 0),
             "legs": out}
@@ -277,6 +286,45 @@ def band_table(cx, objs, w, h, spp, mb, n=8, reps=2, interleaved=False):
             "adj_max_over_mean": round(max(ad) / np.mean(ad), 4)}
 
 
+def graph_line(cx, seed=0, reps=5):
+    """createGraph's integrator (hot path #2, inv_path_trace.cu:152-208) at
+    the reference's own configuration: scenes/0.txt, 500x500, 100 spp, no
+    bounce cap, the reference's target preds/0_true.png; this rank's
+    interleaved rows + one RCCL all-reduce of the fp64 bins.  The host
+    compress (O(nT^2), inv_scene.h:87-115) is not timed."""
+    from inverse_path_tracer_amd import png_read
+
+    gw = gh = 500
+    gspp = 100
+    b, e, st = shard_rows_interleaved(gh, cx.world, cx.rank)
+    sc = Scene(SCENE0)
+    tgt = torch.from_numpy(png_read(GRAPH_TARGET)).to(cx.dev)
+    acc = torch.zeros(((sc.nT + 1) * sc.nT, N.ACC_WIDTH), device=cx.dev, dtype=torch.float64)
+    p = N.make_params(gw, gh, gspp, None, seed, b, e, st)
+
+    def step(i):
+        acc.zero_()
+        N.check(cx.L.ipt_graph_dev(sc.handle, C.byref(p), tgt.data_ptr(), acc.data_ptr(), cx.st))
+        if cx.world > 1:
+            dist.all_reduce(acc)
+
+    step(0)
+    ms = cx.timed(step, reps) / reps
+    frame = gw * gh * gspp
+    flop = frame * CASTS_PER_SAMPLE_GRAPH * sc.nT * FLOP_PER_TEST
+    out = {"value": round(frame / ms / 1e3, 2), "unit": "Msamples/s", "ms_per_step": round(ms, 4),
+           "workload": "createGraph: scenes/0.txt (30 triangles), 500x500, 100 spp, unbounded, target "
+                       "preds/0_true.png; interleaved rows over %d rank(s) + all-reduce of the (nT+1)*nT*8 fp64 "
+                       "bins" % cx.world,
+           "roofline": {"bound": "valu", "unit": "TFLOP/s", "peak": PEAK_FP32_TFLOPS,
+                        "flop_per_sample": round(CASTS_PER_SAMPLE_GRAPH * sc.nT * FLOP_PER_TEST, 1),
+                        "formula": "C_bar(graph, %.4f) * nT(30) * 38, brute-force-equivalent" % CASTS_PER_SAMPLE_GRAPH,
+                        "achieved": round(flop / (ms / 1e3) / 1e12, 3),
+                        "frac": round(flop / (ms / 1e3) / 1e12 / PEAK_FP32_TFLOPS, 4)}}
+    sc.close()
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -336,8 +384,10 @@ def main():
                  "sphere.obj (assets/northstar.txt, 1310 triangles, BVH), 512x512, 64 spp, 4 bounces"),
                 ("bvh_sphere", SPHERE, W, H, SPP, BOUNCES, "Cornell + sphere.obj (1298 triangles, BVH), 512x512, 64 spp, 4 bounces"),
                 ("c4", SCENE0, 1024, 1024, 256, 8, "C4: scenes/0.txt, 1024x1024, 256 spp, 8 bounces")):
-            bb, ee, ss = shard_rows_interleaved(h, world if key != "c4" else 8, rank) if (key != "c4" or world <= 8) \
-                else (0, 0, 1)
+            if key != "c4":
+                bb, ee, ss = shard_rows_interleaved(h, world, rank)
+            else:  # C4: 8 interleaved shares, one per rank; ranks past 8 run none
+                bb, ee, ss = shard_rows_interleaved(h, 8, rank) if rank < 8 else (0, 0, 1)
             leg = Leg(cx, objs, w, h, spp, mb, bb, ee, step=ss)
             leg.fwd(10**6)
             leg.adjoint(10**6)
@@ -373,6 +423,7 @@ def main():
             sys.path.insert(0, os.path.join(ROOT, "tools"))
             import bench_c5
             extra["c5"] = bench_c5.run(scenes=13, steps=20, warmup=3, total=240)  # 240 steps: the convergence record (~2 s)
+        extra["graph"] = graph_line(cx)
     # ---------------------------------------------------------- roofline of the dominant kernel
     band_samples = head.samples_per_call()
     flop_per_launch = band_samples * CASTS_PER_SAMPLE * N_TRIANGLES * FLOP_PER_TEST
@@ -389,22 +440,26 @@ def main():
     if traffic:
         gbs = traffic / (kernel_ms / 1e3) / 1e9
         hbm = {"bytes_per_launch": traffic, "achieved_GBps": round(gbs, 1), "peak_GBps": 8000.0,
-               "frac": round(gbs / 8000.0, 4), "algorithmic_bytes_per_launch": band_samples * 12,
+               "frac": round(gbs / 8000.0, 4), "algorithmic_bytes_per_launch": head.npix * 12,
+               "algorithmic": "the 12 B/pixel HDR output (compulsory)",
                "source": os.path.relpath(PMC_FILE, ROOT)}
     roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
                 "kernel": "trace_kernel<MODE_FWD>", "kernel_ms": round(kernel_ms, 4),
                 "flop_per_launch": flop_per_launch,
                 "grad_achieved": round(grad_achieved, 3), "grad_frac": round(grad_achieved / PEAK_FP32_TFLOPS, 4),
+                "basis": "brute-force-equivalent work (SURVEY.md 8(d) fixed formula): every cast is charged all "
+                         "nT triangle tests, although the culled casts execute ~1/4 of them -- `executed_frac` "
+                         "is the hardware-use figure",
                 "formula": "samples*C_bar(%.4f)*nT(%d)*38 FLOP / kernel time; peak = FP32 vector peak (equal to "
                            "the FP32 MFMA peak on gfx950)" % (CASTS_PER_SAMPLE, N_TRIANGLES)}
     ex = executed_flop_per_sample("cornell", CASTS_PER_SAMPLE, N_TRIANGLES)
-    if ex:  # the culled shadow cast skips pairs no lane can hit: the work actually issued is smaller
+    if ex:  # the culled casts skip pairs no ray can accept: the work actually issued is smaller
         ea = band_samples * ex / (kernel_ms / 1e3) / 1e12
+        roofline["executed_frac"] = round(ea / PEAK_FP32_TFLOPS, 4)
+        roofline["executed_grad_frac"] = round(band_samples * ex / (bwd_ms / args.steps / 1e3) / 1e12 /
+                                               PEAK_FP32_TFLOPS, 4)
         roofline["executed"] = {"flop_per_sample": round(ex, 1), "achieved": round(ea, 3),
-                                "frac": round(ea / PEAK_FP32_TFLOPS, 4),
-                                "grad_frac": round(band_samples * ex / (bwd_ms / args.steps / 1e3) / 1e12 /
-                                                   PEAK_FP32_TFLOPS, 4),
                                 "source": "triangle tests (x38) and slab tests (x12) actually executed, "
                                           "profiles/bvh_stats.json (IPT_BVH_STATS build)"}
     cpu = None

@@ -65,7 +65,9 @@ void setMaterials(void *scenePtr, float *materials);
  * row_begin, row_begin + row_step, ... < row_end are traced (sharding:
  * row_step 1 = a contiguous band, row_step = world = a rank's interleaved
  * share); images and sample buffers hold those rows, in that order.
- * ABI 2 added row_step (ipt_abi_version). */
+ * ABI 2 added row_step; ABI 3 dropped the quantised-node export of
+ * ipt_scene_export_wide (ipt_abi_version).  Bindings must check the version
+ * before passing this struct. */
 typedef struct ipt_params {
   int32_t width, height, spp, max_bounces;
   uint64_t seed;
@@ -75,7 +77,7 @@ typedef struct ipt_params {
 
 const char *ipt_last_error(void);
 void ipt_clear_error(void);
-int ipt_abi_version(void);            /* 2 */
+int ipt_abi_version(void);            /* 3 */
 int ipt_device_count(void);
 /* Diagnostic: bitwise self-test of the kernels' in-range sqrt/division cores
  * against the IEEE operations over n random operands per test; counts[8]
@@ -125,9 +127,8 @@ int ipt_scene_bvh_info(void *scene, int32_t *info8);
 int ipt_scene_export_bvh(void *scene, float *nodes, float *pairs, int32_t *big_idx);
 /* The 8-wide nodes of the cooperative traversal (info8[5] of them): wide
  * receives info8[5]*64 floats (WideNode: per child lo.xyz, hi.xyz, ref bits,
- * pad), qwide info8[5]*36 uint32 (QWideNode: origin xyz float bits, step
- * exponent bytes, per child packed 8-bit bounds, ref, 0); each nullable. */
-int ipt_scene_export_wide(void *scene, float *wide, uint32_t *qwide);
+ * pad; nullable). */
+int ipt_scene_export_wide(void *scene, float *wide);
 /* The shadow rays' potential occluders (bvh.cpp shadow_occluder_masks):
  * masks receives nT * max(nE, 1) words, word [s * nE + e] = the pairs (bit j
  * = triangles 2j, 2j+1) that may occlude a shadow ray from a vertex on

@@ -17,6 +17,8 @@ LIB_PATH = os.environ.get("IPT_AMD_LIB") or os.path.join(_HERE, "lib", "libipt_a
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ipt.h")
 TRI_EXPORT_STRIDE = 57
 ACC_WIDTH = 8
+# include/ipt.h ipt_abi_version(): the Params layout and signatures below are this version's
+ABI_VERSION = 3
 # acceleration modes (include/ipt.h IPT_ACCEL_*)
 ACCEL_AUTO, ACCEL_BRUTE, ACCEL_BVH = 0, 1, 2
 
@@ -103,7 +105,7 @@ SIGNATURES = {
     "ipt_scene_set_accel": (C.c_int, [vp, C.c_int]),
     "ipt_scene_bvh_info": (C.c_int, [vp, C.POINTER(C.c_int32)]),
     "ipt_scene_export_bvh": (C.c_int, [vp, fp, fp, C.POINTER(C.c_int32)]),
-    "ipt_scene_export_wide": (C.c_int, [vp, fp, C.POINTER(C.c_uint32)]),
+    "ipt_scene_export_wide": (C.c_int, [vp, fp]),
     "ipt_closest_hit_host": (C.c_int, [vp, C.c_int64, fp, fp, C.POINTER(C.c_int32), fp, C.POINTER(C.c_int32)]),
     "ipt_closest_hit_dev": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp, vp, vp]),
     "ipt_scene_shadow_masks": (C.c_int, [vp, C.POINTER(C.c_uint32)]),
@@ -127,6 +129,9 @@ def lib():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
+        v = L.ipt_abi_version()
+        if v != ABI_VERSION:  # a stale build would read ipt_params_t / arguments with another layout
+            raise NativeError("%s has ABI %d, this binding needs %d: rebuild it" % (LIB_PATH, v, ABI_VERSION))
         _lib = L
     return _lib
 

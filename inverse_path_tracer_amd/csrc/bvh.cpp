@@ -553,75 +553,6 @@ static bool build_wide(HostScene *S) {
   return true;
 }
 
-// WideNode -> QWideNode: per axis the smallest step 2^e whose grid (origin a
-// multiple of 2^e, every grid value below 2^24 steps from 0, so exact in
-// fp32) spans the children in 255 steps; lo rounded down, hi up.  The result
-// is verified with the kernel's own decode (fmaf(q, 2^e, o)); false if no
-// exponent works (non-finite boxes).
-static bool quantize_wide(const WideNode &W, QWideNode *Q) {
-  std::memset(Q, 0, sizeof *Q);
-  int32_t refs[8];
-  bool used[8];
-  for (int k = 0; k < 8; ++k) {
-    std::memcpy(&refs[k], &W.s[k][6], sizeof(int32_t));
-    used[k] = refs[k] != kWideEmpty;
-  }
-  uint32_t qlo[8][3] = {{0}}, qhi[8][3] = {{0}};
-  for (int a = 0; a < 3; ++a) {
-    double lo = HUGE_VAL, hi = -HUGE_VAL;
-    for (int k = 0; k < 8; ++k)
-      if (used[k]) {
-        lo = std::min(lo, (double)W.s[k][a]);
-        hi = std::max(hi, (double)W.s[k][3 + a]);
-      }
-    if (!(lo <= hi)) lo = hi = 0.0;  // no child: any grid
-    if (!std::isfinite(lo) || !std::isfinite(hi)) return false;
-    const double mag = std::max(std::fabs(lo), std::fabs(hi));
-    int e = mag > 0 ? (int)std::floor(std::log2(mag)) - 22 : -126;
-    e = std::max(e, (int)std::ceil(std::log2(std::max(hi - lo, 1e-300) / 254.0)));
-    bool ok = false;
-    for (int tries = 0; tries < 8 && !ok; ++tries, ++e) {
-      if (e < -126 || e > 127) break;
-      const double st = std::ldexp(1.0, e);
-      const double o = std::floor(lo / st) * st;
-      const float of = (float)o, sf = (float)st;
-      if ((double)of != o) continue;
-      ok = true;
-      for (int k = 0; k < 8 && ok; ++k) {
-        if (!used[k]) continue;
-        const double l = std::floor(((double)W.s[k][a] - o) / st), h = std::ceil(((double)W.s[k][3 + a] - o) / st);
-        if (l < 0 || h > 255 || h < 0) {
-          ok = false;
-          break;
-        }
-        const float dl = std::fma((float)l, sf, of), dh = std::fma((float)h, sf, of);
-        if (!(dl <= W.s[k][a] && dh >= W.s[k][3 + a]) || (double)dl != o + l * st || (double)dh != o + h * st) {
-          ok = false;
-          break;
-        }
-        qlo[k][a] = (uint32_t)l;
-        qhi[k][a] = (uint32_t)h;
-      }
-      if (ok) {
-        Q->o[a] = of;
-        Q->exps |= (uint32_t)(e + 127) << (8 * a);
-      }
-    }
-    if (!ok) return false;
-  }
-  for (int k = 0; k < 8; ++k) {
-    if (!used[k]) {  // empty slot: lo > hi on x (never hit), ref kWideEmpty
-      Q->c[k][0] = 0xffu;
-      Q->c[k][2] = (uint32_t)kWideEmpty;
-      continue;
-    }
-    Q->c[k][0] = qlo[k][0] | qlo[k][1] << 8 | qlo[k][2] << 16 | qhi[k][0] << 24;
-    Q->c[k][1] = qhi[k][1] | qhi[k][2] << 8;
-    Q->c[k][2] = (uint32_t)refs[k];
-  }
-  return true;
-}
-
 bool build_bvh(HostScene *S) {
   S->bvh_nodes.clear();
   S->bvh_pairs.clear();
@@ -768,16 +699,8 @@ bool build_bvh(HostScene *S) {
     std::memcpy(&N.q[3][0], kid, sizeof kid);
   }
   S->bvh_depth = B.max_depth;
-  if (build_wide(S)) {
-    S->bvh_qwide.resize(S->bvh_wide.size());
-    for (size_t i = 0; i < S->bvh_wide.size(); ++i)
-      if (!quantize_wide(S->bvh_wide[i], &S->bvh_qwide[i])) {
-        S->bvh_status = "8-wide node cannot be quantised";
-        S->bvh_qwide.clear();
-        break;
-      }
-  }
-  if (S->bvh_wide.empty() || S->bvh_qwide.size() != S->bvh_wide.size()) {
+  if (!build_wide(S)) S->bvh_wide.clear();  // (build_wide sets bvh_status)
+  if (S->bvh_wide.empty()) {
     S->bvh_nodes.clear();
     S->bvh_pairs.clear();
     S->bvh_big_pairs.clear();

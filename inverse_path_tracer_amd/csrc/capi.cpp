@@ -2,6 +2,7 @@
 // the explicit-parameter API, over the HIP side in ipt_hip.hip.
 #include <cmath>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <ctime>
 #include <string>
@@ -90,7 +91,7 @@ extern "C" {
 
 const char *ipt_last_error(void) { return g_err.c_str(); }
 void ipt_clear_error(void) { g_err.clear(); }
-int ipt_abi_version(void) { return 2; }
+int ipt_abi_version(void) { return 3; }
 int ipt_device_count(void) { return ipt::gpu_device_count(); }
 int ipt_selftest_math(uint64_t n, uint64_t seed, uint64_t *counts) {
   if (!counts) return -1;
@@ -215,13 +216,11 @@ int ipt_scene_export_bvh(void *scene, float *nodes, float *pairs, int32_t *big_i
   if (pairs && !h.bvh_pairs.empty()) std::memcpy(pairs, h.bvh_pairs.data(), h.bvh_pairs.size() * sizeof(ipt::BvhPair));
   return 0;
 }
-int ipt_scene_export_wide(void *scene, float *wide, uint32_t *qwide) {
+int ipt_scene_export_wide(void *scene, float *wide) {
   GpuScene *s = as_scene(scene);
   if (!s) return -1;
   const ipt::HostScene &h = ipt::gpu_host(s);
   if (wide && !h.bvh_wide.empty()) std::memcpy(wide, h.bvh_wide.data(), h.bvh_wide.size() * sizeof(ipt::WideNode));
-  if (qwide && !h.bvh_qwide.empty())
-    std::memcpy(qwide, h.bvh_qwide.data(), h.bvh_qwide.size() * sizeof(ipt::QWideNode));
   return 0;
 }
 int ipt_scene_shadow_masks(void *scene, uint32_t *masks) {
@@ -236,6 +235,23 @@ int ipt_scene_set_accel(void *scene, int mode) {
   if (!s) return -1;
   return gpu_status(ipt::gpu_set_accel(s, mode));
 }
+// The probe kernel indexes emitter and occluder-mask tables with these: a
+// target >= 0 must be an emitter triangle, a source must lie in [-1, nT).
+static bool probe_ids_ok(GpuScene *s, int64_t n, const int32_t *targets, const int32_t *sources, const char *who) {
+  const ipt::HostScene &h = ipt::gpu_host(s);
+  for (int64_t i = 0; i < n; ++i) {
+    if (targets && targets[i] >= 0 &&
+        std::find(h.emit_tri.begin(), h.emit_tri.end(), targets[i]) == h.emit_tri.end()) {
+      fail(std::string(who) + ": target " + std::to_string(targets[i]) + " is not an emitter triangle");
+      return false;
+    }
+    if (sources && (sources[i] < -1 || sources[i] >= h.nT)) {
+      fail(std::string(who) + ": source " + std::to_string(sources[i]) + " outside [-1, nT)");
+      return false;
+    }
+  }
+  return true;
+}
 int ipt_closest_hit_host(void *scene, int64_t n, const float *origins, const float *dirs, const int32_t *targets,
                          float *t, int32_t *idx) {
   GpuScene *s = as_scene(scene);
@@ -243,6 +259,7 @@ int ipt_closest_hit_host(void *scene, int64_t n, const float *origins, const flo
     if (s) fail("ipt_closest_hit_host: bad arguments");
     return -1;
   }
+  if (!probe_ids_ok(s, n, targets, nullptr, "ipt_closest_hit_host")) return -1;
   return gpu_status(ipt::gpu_closest_hit_host(s, n, origins, dirs, targets, nullptr, t, idx));
 }
 int ipt_shadow_hit_host(void *scene, int64_t n, const float *origins, const float *dirs, const int32_t *targets,
@@ -252,6 +269,7 @@ int ipt_shadow_hit_host(void *scene, int64_t n, const float *origins, const floa
     if (s) fail("ipt_shadow_hit_host: bad arguments");
     return -1;
   }
+  if (!probe_ids_ok(s, n, targets, sources, "ipt_shadow_hit_host")) return -1;
   return gpu_status(ipt::gpu_closest_hit_host(s, n, origins, dirs, targets, sources, t, idx));
 }
 int ipt_closest_hit_dev(void *scene, int64_t n, const float *origins_dev, const float *dirs_dev,

@@ -326,9 +326,6 @@ __device__ __forceinline__ V3 unit_in_range(V3 v) { return div3_core(v, sqrt_cor
 // evaluated branch-free per lane and committed with a select.  Each skip
 // condition is written exactly as the reference's (negated) so NaNs take the
 // same branch.
-#ifndef IPT_UNROLL2
-#define IPT_UNROLL2 0
-#endif
 // One triangle of the closest-hit loop: branch-free test, select on accept.
 __device__ __forceinline__ void hit_test(const TriIsect &T, int i, V3 p, V3 d, float &bt, int &bi) {
   const float denom = fmaf(T.n[2], d.z, fmaf(T.n[1], d.y, T.n[0] * d.x));
@@ -345,42 +342,6 @@ __device__ __forceinline__ void hit_test(const TriIsect &T, int i, V3 p, V3 d, f
   bi = take ? i : bi;
 }
 
-__device__ __forceinline__ int closest_hit(const TriIsect *__restrict__ tris, int nT, V3 p, V3 d,
-                                           float &best_t) {
-  float bt = __builtin_inff();
-  int bi = -1;
-  // Software pipeline: the scalar loads of the next record(s) are issued
-  // before the tests of the current one(s) -- SMEM returns out of order, so
-  // every wait is a full lgkmcnt(0) and must be covered by VALU work.
-#if IPT_UNROLL2
-  TriIsect A = tris[0], B = tris[nT > 1 ? 1 : 0];
-  int i = 0;
-  for (; i + 1 < nT; i += 2) {
-    const TriIsect cA = A, cB = B;
-    A = tris[i + 2 < nT ? i + 2 : nT - 1];
-    B = tris[i + 3 < nT ? i + 3 : nT - 1];
-    hit_test(cA, i, p, d, bt, bi);      // order kept: strict '<' prefers the first
-    hit_test(cB, i + 1, p, d, bt, bi);
-  }
-  if (i < nT) hit_test(A, i, p, d, bt, bi);
-#else
-  TriIsect nxt = tris[0];
-  for (int i = 0; i < nT; ++i) {
-    const TriIsect T = nxt;
-    nxt = tris[i + 1 < nT ? i + 1 : i];
-    hit_test(T, i, p, d, bt, bi);
-  }
-#endif
-  best_t = bt;
-  return bi;
-}
-
-#ifndef IPT_PAIRS
-#define IPT_PAIRS 1
-#endif
-#ifndef IPT_PAIR_UNROLL
-#define IPT_PAIR_UNROLL 1
-#endif
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f2 bc2(float x) { return f2{x, x}; }
@@ -491,34 +452,7 @@ __device__ __forceinline__ void hit_test_pair(const TriPair &T, int i, V3 p, V3 
 // each costs two v_mov; from LDS (immediate offsets) it costs no VALU.  The
 // unrolled triangle index is an inline constant (no v_mov either).
 constexpr int kSmallPairs = 16;
-// IPT_FAST_CAST=1 (tolerance-mode A/B build, NOT bit-exact): the small-scene
-// loop computes t = num * rcp(-denom) (the 1-ulp reciprocal without the
-// Newton / residual steps of the IEEE division), num = p.n + cn with cn =
-// -(c.n) precomputed per triangle (LDS, after the plane offsets), and drops
-// the |n.d| >= 1e-4 test (a near-parallel plane gives |t| huge or NaN, which
-// the other tests reject but for rare grazing hits): 33 instead of 45 VALU
-// per pair.  Off: the parity build is the product.
-#ifndef IPT_FAST_CAST
-#define IPT_FAST_CAST 0
-#endif
-constexpr int kE3Floats = IPT_FAST_CAST ? 8 : 6;  // LDS floats per pair: 3 plane offsets x 2 (+ cn x 2)
-__device__ __forceinline__ void pair_ray_fast(const TriPair &T, f2 cn, int ia, int ib, V3 p, V3 d, float &bt, int &bi,
-                                              f2 e03, f2 e13, f2 e23) {
-  const f2 n0 = ld2(T, 3), n1 = ld2(T, 4), n2 = ld2(T, 5);
-  const f2 num = fma2(bc2(p.z), n2, fma2(bc2(p.y), n1, fma2(bc2(p.x), n0, cn)));
-  const f2 denom = fma2(n2, bc2(d.z), fma2(n1, bc2(d.y), n0 * bc2(d.x)));
-  const f2 t = num * f2{__builtin_amdgcn_rcpf(-denom.x), __builtin_amdgcn_rcpf(-denom.y)};
-  const f2 qx = fma2(bc2(d.x), t, bc2(p.x)), qy = fma2(bc2(d.y), t, bc2(p.y)), qz = fma2(bc2(d.z), t, bc2(p.z));
-  const f2 s0 = fma2(qz, ld2(T, 8), fma2(qy, ld2(T, 7), fma2(qx, ld2(T, 6), e03)));
-  const f2 s1 = fma2(qz, ld2(T, 12), fma2(qy, ld2(T, 11), fma2(qx, ld2(T, 10), e13)));
-  const f2 s2 = fma2(qz, ld2(T, 16), fma2(qy, ld2(T, 15), fma2(qx, ld2(T, 14), e23)));
-  const bool ta = (t.x >= kEpsUp) & (t.x < bt) & !(fmaxf(fmaxf(s0.x, s1.x), s2.x) > 0.f);
-  bt = ta ? t.x : bt;
-  bi = ta ? ia : bi;
-  const bool tb = (t.y >= kEpsUp) & (t.y < bt) & !(fmaxf(fmaxf(s0.y, s1.y), s2.y) > 0.f);
-  bt = tb ? t.y : bt;
-  bi = tb ? ib : bi;
-}
+constexpr int kE3Floats = 6;  // LDS floats per pair: 3 plane offsets x 2
 __device__ __forceinline__ int closest_hit_pairs_small(const TriPair *__restrict__ pairs, const f2 *e3, int nT,
                                                        V3 p, V3 d, float &best_t) {
   float bt = __builtin_inff();
@@ -540,11 +474,7 @@ __device__ __forceinline__ int closest_hit_pairs_small(const TriPair *__restrict
   for (int j = 0; j < kSmallPairs; ++j) {
     if (j < nP) {  // wave-uniform
       const TriPair T = pairs[j];
-#if IPT_FAST_CAST
-      pair_ray_fast(T, e3l[4 * j + 3], 2 * j, 2 * j + 1, p, d, bt, bi, e3l[4 * j], e3l[4 * j + 1], e3l[4 * j + 2]);
-#else
       pair_ray(T, pair_origin(T, p), 2 * j, 2 * j + 1, p, d, bt, bi, e3l[3 * j], e3l[3 * j + 1], e3l[3 * j + 2]);
-#endif
     }
   }
   best_t = bt;
@@ -556,40 +486,24 @@ __device__ __forceinline__ int closest_hit_pairs(const TriPair *__restrict__ pai
   float bt = __builtin_inff();
   int bi = -1;
   const int nP = (nT + 1) >> 1;
-#if IPT_PAIR_UNROLL == 2
-  int j = 0;
-  for (; j + 1 < nP; j += 2) {
-    const TriPair A = pairs[j], B = pairs[j + 1];
-    hit_test_pair(A, 2 * j, p, d, bt, bi);
-    hit_test_pair(B, 2 * j + 2, p, d, bt, bi);
-  }
-  if (j < nP) hit_test_pair(pairs[j], 2 * j, p, d, bt, bi);
-#else
   TriPair nxt = pairs[0];
   for (int j = 0; j < nP; ++j) {
     const TriPair T = nxt;
     nxt = pairs[j + 1 < nP ? j + 1 : j];
     hit_test_pair(T, 2 * j, p, d, bt, bi);
   }
-#endif
   best_t = bt;
   return bi;
 }
 
 // ------------------------------------------------------------ BVH closest hit
 // Exact replacement of the brute-force loop for large scenes (bvh.cpp states
-// why): per-lane stack traversal of the binary BVH, one ray per lane.  Node
-// boxes come from the workgroup's LDS copy (or global memory when the tree is
-// too big to stage), leaf triangle pairs through per-lane vector loads; the
-// leaf test is pair_ray's arithmetic, with the accept step keeping the
-// lexicographic minimum of (t, original triangle index) -- the result of the
-// reference's in-order strict-'<' loop, whatever order the leaves come in.
+// why): a per-lane pre-pass over the large triangles, then the cooperative
+// traversal of the 8-wide tree below; every accept keeps the lexicographic
+// minimum of (t, original triangle index) -- the result of the reference's
+// in-order strict-'<' loop, whatever order the triangles come in.
 struct BvhView {
-  const BvhNode *nodes;     // global copy
-  const float4 *lnodes;     // LDS copy (nullptr: read `nodes`)
-  const BvhPair *pairs;
   const TriIsect *isect;    // original-order records (shadow target test)
-  uint32_t *stack;          // LDS, entry k of this lane at stack[k * kStride]
   // brute-force pre-pass over the large triangles (bvh.cpp kBigFrac)
   const TriPair *big;
   const int32_t *big_idx;   // original indices, 2 per pair
@@ -599,7 +513,6 @@ struct BvhView {
   const float *big_lds;       // LDS copy of the pairs + their indices (culled path pre-pass), or nullptr
   const float *emit_is;       // LDS copy of the emitters' TriIsect records (shadow target test), or nullptr
 };
-constexpr int kStackStride = 256;  // = the megakernel's block size
 constexpr int kBvhDone = (int)0x80000000;
 // Profiling build (make variant DEFS=-DIPT_BVH_STATS): work counters summed
 // over all lanes (ipt_debug_bvh_stats) -- the "tests actually executed" of
@@ -612,56 +525,6 @@ constexpr int kBvhStats = 23;  // [12..17]: culled shadow casts (shadow_hit_pair
 #ifdef IPT_BVH_STATS
 __device__ unsigned long long g_bvh_stats[kBvhStats];
 #endif
-
-__device__ __forceinline__ void bvh_load_node(const BvhView &B, int n, float4 &q0, float4 &q1, float4 &q2,
-                                              float4 &q3) {
-  if (B.lnodes) {
-    const float4 *s = B.lnodes + 4 * n;
-    q0 = s[0];
-    q1 = s[1];
-    q2 = s[2];
-    q3 = s[3];
-  } else {
-    const float4 *s = reinterpret_cast<const float4 *>(B.nodes + n);
-    q0 = s[0];
-    q1 = s[1];
-    q2 = s[2];
-    q3 = s[3];
-  }
-}
-
-// One leaf pair with per-lane operands; accept = valid && (t, i) < (bt, bi).
-__device__ __forceinline__ void bvh_pair_test(const BvhPair &T, V3 p, V3 d, float &bt, int &bi) {
-  const f2 c0 = f2{T.f[0][0], T.f[0][1]}, c1 = f2{T.f[1][0], T.f[1][1]}, c2 = f2{T.f[2][0], T.f[2][1]};
-  const f2 n0 = f2{T.f[3][0], T.f[3][1]}, n1 = f2{T.f[4][0], T.f[4][1]}, n2 = f2{T.f[5][0], T.f[5][1]};
-  const f2 px = bc2(p.x) - c0, py = bc2(p.y) - c1, pz = bc2(p.z) - c2;
-  const f2 num = fma2(pz, n2, fma2(py, n1, px * n0));
-  const f2 denom = fma2(n2, bc2(d.z), fma2(n1, bc2(d.y), n0 * bc2(d.x)));
-  const f2 nb = denom;
-  const f2 r0 = f2{__builtin_amdgcn_rcpf(-denom.x), __builtin_amdgcn_rcpf(-denom.y)};
-  const f2 e0 = fma2(nb, r0, bc2(1.0f));
-  const f2 r1 = fma2(e0, r0, r0);
-  const f2 q0 = num * r1;
-  const f2 e1 = fma2(nb, q0, num);
-  const f2 q1 = fma2(e1, r1, q0);
-  const f2 e2 = fma2(nb, q1, num);
-  const f2 t = fma2(e2, r1, q1);
-  const f2 qx = fma2(bc2(d.x), t, bc2(p.x)), qy = fma2(bc2(d.y), t, bc2(p.y)), qz = fma2(bc2(d.z), t, bc2(p.z));
-  const f2 s0 = fma2(qz, f2{T.f[8][0], T.f[8][1]}, fma2(qy, f2{T.f[7][0], T.f[7][1]},
-                                                        fma2(qx, f2{T.f[6][0], T.f[6][1]}, f2{T.f[9][0], T.f[9][1]})));
-  const f2 s1 = fma2(qz, f2{T.f[12][0], T.f[12][1]}, fma2(qy, f2{T.f[11][0], T.f[11][1]},
-                                                          fma2(qx, f2{T.f[10][0], T.f[10][1]}, f2{T.f[13][0], T.f[13][1]})));
-  const f2 s2 = fma2(qz, f2{T.f[16][0], T.f[16][1]}, fma2(qy, f2{T.f[15][0], T.f[15][1]},
-                                                          fma2(qx, f2{T.f[14][0], T.f[14][1]}, f2{T.f[17][0], T.f[17][1]})));
-  const bool va = !(fabsf(denom.x) < kMinDotUp) && !(t.x < kEpsUp) && !(s0.x > 0.f) && !(s1.x > 0.f) && !(s2.x > 0.f);
-  const bool ta = va & ((t.x < bt) | ((t.x == bt) & (T.idx[0] < bi)));
-  bt = ta ? t.x : bt;
-  bi = ta ? T.idx[0] : bi;
-  const bool vb = !(fabsf(denom.y) < kMinDotUp) && !(t.y < kEpsUp) && !(s0.y > 0.f) && !(s1.y > 0.f) && !(s2.y > 0.f);
-  const bool tb = vb & ((t.y < bt) | ((t.y == bt) & (T.idx[1] < bi)));
-  bt = tb ? t.y : bt;
-  bi = tb ? T.idx[1] : bi;
-}
 
 // The large triangles, unrolled like closest_hit_pairs_small (scalar-loaded
 // pairs, plane offsets from LDS) with the lexicographic accept.
@@ -742,14 +605,6 @@ __device__ __forceinline__ SlabRay slab_ray(V3 p, V3 d) {
 // emitter (static potential-occluder masks, bvh.cpp shadow_occluder_masks)
 #ifndef IPT_SHADOW_PO
 #define IPT_SHADOW_PO 1
-#endif
-// IPT_SHADOW_TARGET_PAIR=1: the culled shadow cast tests the target with its
-// pair partner (gathered from the path cull's LDS pair copy), see
-// shadow_hit_pairs_small.  Measured slower (C2 forward 1.68 -> 1.83 ms): the
-// 36 gathered floats, live next to the shading state, spill 44-48 B per lane
-// (profiles/r02_variants_shadow_target_pair.log).  Off.
-#ifndef IPT_SHADOW_TARGET_PAIR
-#define IPT_SHADOW_TARGET_PAIR 0
 #endif
 typedef __attribute__((address_space(3))) const uint32_t lds_u32c;
 // Bit j: the ray enters pair j's acceptance box within [kEpsUp, bt] (the
@@ -835,25 +690,14 @@ __device__ __forceinline__ TriPair load_pair_lds(const lds_f32 *pl, int j) {
   }
   return T;
 }
-// pairs_lds (the culled path cast's TriPair copy, or nullptr): the target is
-// decided together with its pair partner -- the in-order loop over the
-// target's own pair from the empty state (packed, gathered per lane), which
-// also settles whether the partner occludes or ties ahead of it -- and that
-// pair leaves the occlusion pass.
+// The target's record comes from the workgroup's LDS copy of the TriIsect array.
 __device__ __forceinline__ int shadow_hit_pairs_small(const lds_f32 *isect_lds, const TriPair *__restrict__ pairs,
                                                       const PairBox2 *__restrict__ boxes, const f2 *e3, int nT, V3 p,
-                                                      V3 d, int target, float &best_t, uint32_t allow = 0xffffffffu,
-                                                      const lds_f32 *pairs_lds = nullptr) {
+                                                      V3 d, int target, float &best_t, uint32_t allow = 0xffffffffu) {
   float bt = __builtin_inff();
   int bi = -1;
   bool live;
-  if (pairs_lds) {
-    const int jt = target >> 1;
-    const TriPair T = load_pair_lds(pairs_lds, jt);
-    pair_ray(T, pair_origin(T, p), 2 * jt, 2 * jt + 1, p, d, bt, bi, ld2(T, 9), ld2(T, 13), ld2(T, 17));
-    live = bi == target;
-    allow &= ~(1u << jt);
-  } else {  // the target's record from the LDS copy of the TriIsect array
+  {
     TriIsect T;
     float *tf = reinterpret_cast<float *>(&T);
     const lds_f32 *q = isect_lds + 20 * target;
@@ -938,25 +782,6 @@ __device__ __forceinline__ int closest_hit_pairs_culled(const lds_f32 *pairs_lds
   }
   best_t = bt;
   return bi;
-}
-
-// Both children's boxes of an inner node against [0, bt]: h0/h1 = hit,
-// en0/en1 = entry parameters, c0/c1 = child links.
-__device__ __forceinline__ void bvh_node_test(const BvhView &B, int node, const SlabRay &r, float bt, bool &h0,
-                                              bool &h1, float &en0, float &en1, int &c0, int &c1) {
-  float4 q0, q1, q2, q3;
-  bvh_load_node(B, node, q0, q1, q2, q3);
-  const f2 tx0 = fma2(f2{q0.x, q1.z}, r.ix, r.ox), tx1 = fma2(f2{q0.y, q1.w}, r.ix, r.ox);
-  const f2 ty0 = fma2(f2{q0.z, q2.x}, r.iy, r.oy), ty1 = fma2(f2{q0.w, q2.y}, r.iy, r.oy);
-  const f2 tz0 = fma2(f2{q1.x, q2.z}, r.iz, r.oz), tz1 = fma2(f2{q1.y, q2.w}, r.iz, r.oz);
-  en0 = fmaxf(fmaxf(fminf(tx0.x, tx1.x), fminf(ty0.x, ty1.x)), fmaxf(fminf(tz0.x, tz1.x), 0.f));
-  const float ex0 = fminf(fminf(fmaxf(tx0.x, tx1.x), fmaxf(ty0.x, ty1.x)), fminf(fmaxf(tz0.x, tz1.x), bt));
-  en1 = fmaxf(fmaxf(fminf(tx0.y, tx1.y), fminf(ty0.y, ty1.y)), fmaxf(fminf(tz0.y, tz1.y), 0.f));
-  const float ex1 = fminf(fminf(fmaxf(tx0.y, tx1.y), fmaxf(ty0.y, ty1.y)), fminf(fmaxf(tz0.y, tz1.y), bt));
-  h0 = en0 <= ex0;
-  h1 = en1 <= ex1;
-  c0 = __float_as_int(q3.x);
-  c1 = __float_as_int(q3.y);
 }
 
 // The large-triangle pre-pass of a path ray with closest_hit_pairs_culled's
@@ -1060,86 +885,6 @@ __device__ __forceinline__ bool bvh_prepass(const BvhView &B, V3 p, V3 d, float 
   return true;
 }
 
-// Does the ray reach either child of the root within [0, bt]?  (If not, the
-// traversal cannot change (bt, bi).)
-__device__ __forceinline__ bool bvh_root_test(const BvhView &B, V3 p, V3 d, float bt) {
-  bool h0, h1;
-  float en0, en1;
-  int c0, c1;
-  bvh_node_test(B, 0, slab_ray(p, d), bt, h0, h1, en0, en1, c0, c1);
-  return h0 || h1;
-}
-
-// The traversal proper from the root, continuing the lexicographic minimum
-// (bt, bi).  SHADOW: stops as soon as bi is no longer `target` (occluded).
-template <bool SHADOW, int STRIDE = kStackStride>
-__device__ __forceinline__ void bvh_traverse(const BvhView &B, V3 p, V3 d, float &bt, int &bi, int target) {
-  const SlabRay r = slab_ray(p, d);
-  uint32_t *stk = B.stack;
-  int sp = 0;
-  int node = 0;
-#ifdef IPT_BVH_STATS
-  uint32_t st_nodes = 0, st_pairs = 0;
-#endif
-  while (node != kBvhDone) {
-    while (node >= 0) {  // inner node: test both children's boxes
-#ifdef IPT_BVH_STATS
-      ++st_nodes;
-#endif
-      bool h0, h1;
-      float en0, en1;
-      int c0, c1;
-      bvh_node_test(B, node, r, bt, h0, h1, en0, en1, c0, c1);
-      if (h0 && h1) {
-        const bool first0 = en0 <= en1;
-        stk[sp * STRIDE] = (uint32_t)(first0 ? c1 : c0);
-        ++sp;
-        node = first0 ? c0 : c1;
-      } else if (h0 || h1) {
-        node = h0 ? c0 : c1;
-      } else {
-        node = sp > 0 ? (int)stk[--sp * STRIDE] : kBvhDone;
-      }
-    }
-    if (node != kBvhDone) {  // leaf
-      const int code = ~node;
-      const int first = code >> kBvhLeafPairBits, np = (code & ((1 << kBvhLeafPairBits) - 1)) + 1;
-      for (int j = 0; j < np; ++j) bvh_pair_test(B.pairs[first + j], p, d, bt, bi);
-#ifdef IPT_BVH_STATS
-      st_pairs += np;
-#endif
-      node = sp > 0 ? (int)stk[--sp * STRIDE] : kBvhDone;
-      if (SHADOW && bi != target) node = kBvhDone;  // occluded: decided
-    }
-  }
-#ifdef IPT_BVH_STATS
-  atomicAdd(&g_bvh_stats[0], 1ull);
-  atomicAdd(&g_bvh_stats[1], (unsigned long long)st_nodes);
-  atomicAdd(&g_bvh_stats[2], (unsigned long long)st_pairs);
-  if (SHADOW && bi != target) atomicAdd(&g_bvh_stats[3], 1ull);
-#endif
-}
-
-// Closest hit through the BVH, one lane per ray.  target < 0: ordinary cast.
-// target >= 0 (next-event shadow ray towards emitter triangle `target`): the
-// caller only needs to know whether the closest hit IS `target` (and its t),
-// so the target is tested first, its (t, index) seeds the search -- pruning
-// every box beyond it -- and the first triangle found ahead of it ends the
-// traversal (result != target, exactly as the full search would conclude).
-// Returns the hit's original triangle index or -1.
-template <bool SHADOW>
-__device__ __forceinline__ int closest_hit_bvh(const BvhView &B, V3 p, V3 d, float &best_t, int target = -1) {
-  float bt;
-  int bi;
-  if (bvh_prepass<SHADOW>(B, p, d, bt, bi, target)) {
-#ifndef IPT_ABL_NOTRAV  // timing-only ablation build: pre-pass only, no traversal
-    bvh_traverse<SHADOW>(B, p, d, bt, bi, target);
-#endif
-  }
-  best_t = bt;
-  return bi;
-}
-
 // ------------------------------------------------------------ cooperative BVH traversal
 // The per-lane traversal above is latency-bound: the ~10% of lanes whose ray
 // reaches the tree each walk ~13 dependent node/leaf steps while the rest of
@@ -1152,34 +897,31 @@ __device__ __forceinline__ int closest_hit_bvh(const BvhView &B, V3 p, V3 d, flo
 // All lanes of a group hold identical copies of the ray state, so every
 // branch is group-uniform and the DPP reductions (xor 1, xor 2 within quads,
 // half-row mirror) only read lanes of the same, active group.
-// IPT_BVH_QNODES=1: the traversal reads QWideNode (144 B, 9 float4) instead
-// of WideNode (256 B, 16 float4), so the northstar tree (143 nodes) fits the
-// LDS stage; decoding costs ~18 VALU per lane and visit.  Measured SLOWER
-// (profiles/r02_variants_qnodes.log, C2 size: sphere 6.96 -> 7.41 ms,
-// northstar 8.80 -> 9.04 ms even though its nodes move from L2 to LDS): the
-// cooperative traversal is issue-bound, not fetch-latency-bound.  Off.
-#ifndef IPT_BVH_QNODES
-#define IPT_BVH_QNODES 0
-#endif
-constexpr int kWideF4 = IPT_BVH_QNODES ? 9 : 16;  // float4 per wide node
-// IPT_BVH_OCTANT=1 (default): lane j of a group tests the child of rank j in
-// the ray octant's precomputed front-to-back order (bvh.cpp, slot o's pad
-// word), so the next node is the lowest set bit of the hit mask -- no DPP
-// distance reduction per visit (~15 VALU), one extra dependent LDS read.
-// Exact either way (the visit order never changes the lexicographic result);
-// sphere scene forward 7.04 -> 6.69 ms, north-star 8.90 -> 8.57 ms
-// (profiles/r02_variants_octant.log).
-#ifndef IPT_BVH_OCTANT
-#define IPT_BVH_OCTANT 1
-#endif
+constexpr int kWideF4 = 16;  // float4 per wide node (WideNode, 256 B)
+// Lane j of a group tests the child of rank j in the ray octant's
+// precomputed front-to-back order (bvh.cpp, slot o's pad word), so the next
+// node is the lowest set bit of the hit mask -- no DPP distance reduction per
+// visit (~15 VALU), one extra dependent LDS read.  Exact either way (the
+// visit order never changes the lexicographic result); sphere scene forward
+// 7.04 -> 6.69 ms, north-star 8.90 -> 8.57 ms (profiles/r02_variants_octant.log).
 struct CoopView {
-  const float4 *wn;    // wide nodes (WideNode or QWideNode, kWideF4 float4 each)
+  const float4 *wn;    // wide nodes (WideNode, kWideF4 float4 each)
   bool wn_lds;         // wn points into LDS (else global memory)
   const TriIsect *wt;  // leaf triangles, pad[0] = original index
   uint32_t *stk;       // LDS: this wave's 8 group stacks, `stride` entries each
   int stride;
   float root[6];       // the tree's box: lo xyz, hi xyz
 };
+
+// Whole-wave neighbour shifts (GFX9 DPP wave_shr:1 / wave_shl:1, one VALU
+// move): lane i receives lane i-1's (shr) or lane i+1's (shl) value; lane 0
+// (shr) / lane 63 (shl) receive 0 -- callers never consume those.
+__device__ __forceinline__ float wave_shr1(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float wave_shl1(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
 
 template <int CTRL>
 __device__ __forceinline__ void lexmin_dpp(float &t, int &i) {
@@ -1264,8 +1006,7 @@ __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3
     if (src >= 0) {
       const int target = gi;
       const SlabRay r = slab_ray(gp, gd);
-      const int oct = (gd.x < 0.f ? 1 : 0) | (gd.y < 0.f ? 2 : 0) | (gd.z < 0.f ? 4 : 0);  // IPT_BVH_OCTANT
-      (void)oct;
+      const int oct = (gd.x < 0.f ? 1 : 0) | (gd.y < 0.f ? 2 : 0) | (gd.z < 0.f ? 4 : 0);
       uint32_t *stk = C.stk + g * C.stride;
       int node = 0, sp = 0;
 #ifdef IPT_BVH_STATS
@@ -1276,28 +1017,6 @@ __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3
 #ifdef IPT_BVH_STATS
           ++st_nodes;
 #endif
-#if IPT_BVH_QNODES
-          // QWideNode: header (grid origin, step exponents) + this lane's child
-          v4f hd, ch;
-          if (C.wn_lds) {  // typed per branch: ds_read_b128, not a flat load
-            const lds_v4 *q = (const lds_v4 *)C.wn + kWideF4 * node;
-            hd = q[0];
-            ch = q[1 + j];
-          } else {
-            const gbl_v4 *q = (const gbl_v4 *)C.wn + kWideF4 * node;
-            hd = q[0];
-            ch = q[1 + j];
-          }
-          const uint32_t eb = __float_as_uint(hd.w);
-          const float sx = __uint_as_float((eb & 0xffu) << 23), sy = __uint_as_float(((eb >> 8) & 0xffu) << 23);
-          const float sz = __uint_as_float(((eb >> 16) & 0xffu) << 23);
-          const uint32_t w0 = __float_as_uint(ch.x), w1 = __float_as_uint(ch.y);
-          // o + q * 2^e: exact (scene_layout.h), so these are the grid boxes themselves
-          const float4 a = make_float4(fmaf((float)(w0 & 0xffu), sx, hd.x), fmaf((float)((w0 >> 8) & 0xffu), sy, hd.y),
-                                       fmaf((float)((w0 >> 16) & 0xffu), sz, hd.z), fmaf((float)(w0 >> 24), sx, hd.x));
-          const float4 b = make_float4(fmaf((float)(w1 & 0xffu), sy, hd.y), fmaf((float)((w1 >> 8) & 0xffu), sz, hd.z),
-                                       ch.z, 0.f);
-#elif IPT_BVH_OCTANT
           // lane j tests the child of rank j in the ray octant's front-to-back order
           float4 a, b;
           if (C.wn_lds) {  // typed per branch: ds_read_b128, not a flat load
@@ -1315,20 +1034,6 @@ __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3
             a = make_float4(qa.x, qa.y, qa.z, qa.w);
             b = make_float4(qb.x, qb.y, qb.z, qb.w);
           }
-#else
-          float4 a, b;
-          if (C.wn_lds) {  // typed per branch: ds_read_b128, not a flat load
-            const lds_v4 *q = (const lds_v4 *)C.wn + 2 * (8 * node + j);
-            const v4f qa = q[0], qb = q[1];
-            a = make_float4(qa.x, qa.y, qa.z, qa.w);
-            b = make_float4(qb.x, qb.y, qb.z, qb.w);
-          } else {
-            const gbl_v4 *q = (const gbl_v4 *)C.wn + 2 * (8 * node + j);
-            const v4f qa = q[0], qb = q[1];
-            a = make_float4(qa.x, qa.y, qa.z, qa.w);
-            b = make_float4(qb.x, qb.y, qb.z, qb.w);
-          }
-#endif
           const int ref = __float_as_int(b.z);
           const float tx0 = fmaf(a.x, r.ix.x, r.ox.x), tx1 = fmaf(a.w, r.ix.x, r.ox.x);
           const float ty0 = fmaf(a.y, r.iy.x, r.oy.x), ty1 = fmaf(b.x, r.iy.x, r.oy.x);
@@ -1339,7 +1044,7 @@ __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3
           const uint32_t hm = (uint32_t)(__ballot(h) >> (lane & 56)) & 0xffu;
           if (hm == 0) {
             node = sp > 0 ? (int)stk[--sp] : kBvhDone;
-          } else if (IPT_BVH_OCTANT && !IPT_BVH_QNODES) {
+          } else {
             // next = the nearest-ranked hit child; the other hits are pushed
             // farthest first, so they pop in front-to-back order
             const int f = __builtin_ctz(hm);
@@ -1348,15 +1053,6 @@ __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3
             if ((others >> j) & 1u) stk[sp + __popc(others >> (j + 1))] = (uint32_t)ref;
             sp += __popc(others);
             node = nx;
-          } else {
-            float ek = h ? en : __builtin_inff();
-            int rk = h ? ref : 0x7fffffff;
-            group_lexmin(ek, rk);  // nearest hit child (ties: smaller ref)
-            const bool other = h && ref != rk;
-            const uint32_t om = (uint32_t)(__ballot(other) >> (lane & 56)) & 0xffu;
-            if (other) stk[sp + __popc(om & ((1u << j) - 1u))] = (uint32_t)ref;
-            sp += __popc(om);
-            node = rk;
           }
         } else {  // leaf: lane j tests triangle j (8 per round)
 #ifdef IPT_BVH_STATS

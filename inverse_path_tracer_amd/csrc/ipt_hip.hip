@@ -70,19 +70,12 @@ constexpr bool is_adj() {
 constexpr int kBlock = 256;
 // Adjoint vertex record (per lane, in LDS): tri | et << 16, the emitter factor
 // s (lo = Ke[et] * s is rebuilt bit-identically in the sweep; s = 0 when the
-// shadow ray failed), coeff; with a Phong lobe also specd and speci.
-// With IPT_ADJ_STORE_M the record also keeps the vertex's prefix throughput
-// M (the forward's own value), so the sweep is O(K) instead of recomputing
-// every prefix product (O(K^2)); costs 3 words per vertex of LDS.  Measured
-// with the wave sweep reading it, at 5 waves/SIMD: C2 adjoint 2.41 -> 2.66 ms
-// (2.59 without the camera-ray ring, which keeps 5 blocks per CU), scenes/0
-// 2.95 -> 3.20 (profiles/r02_variants_adj_sweep.log) -- off by default.
-#ifndef IPT_ADJ_STORE_M
-#define IPT_ADJ_STORE_M 0
-#endif
-constexpr int kRecM = 3;                                   // M.x at field 3 (if stored)
-constexpr int kRecSD = IPT_ADJ_STORE_M ? 6 : 3;            // specd, then speci
-constexpr int kRecFieldsDiffuse = IPT_ADJ_STORE_M ? 6 : 3;
+// shadow ray failed), coeff; with a Phong lobe also specd and speci.  The
+// prefix throughputs are not recorded (3 more words per vertex cost a wave
+// of occupancy and measured slower, profiles/r02_variants_adj_sweep.log):
+// the sweep rebuilds them with the forward's own operations.
+constexpr int kRecSD = 3;  // specd, then speci
+constexpr int kRecFieldsDiffuse = 3;
 constexpr int kRecFieldsSpec = kRecFieldsDiffuse + 2;
 constexpr int kMaxAdjTris = 65535;  // tri and et share one 32-bit field
 constexpr int kEdgeW = 8;      // graph bin: w, w*f, pix[3]*w*f, light[3]*w*f
@@ -158,7 +151,6 @@ struct TraceArgs {
   uint64_t m_spp, m_W, m_npix;
   // BVH (BVH instances only): nodes staged in LDS (0: read from global),
   // traversal stack entries per lane
-  int bvh_lds_nodes, bvh_stack;
   int bvh_nbig;                 // large-triangle pairs tested before the traversal
   // cooperative traversal (IPT_BVH_COOP): 8-wide nodes (first bvh_wide_lds of
   // them staged in LDS: all or none), leaf triangles, group-stack entries
@@ -328,73 +320,39 @@ constexpr int min_blocks() {
   return BVH ? (is_adj<MODE>() ? IPT_MIN_BLOCKS_BVH_ADJ : (MODE == 0 ? IPT_MIN_BLOCKS_BVH_FWD : IPT_MIN_BLOCKS_BVH))
              : (MODE == 0 ? IPT_MIN_BLOCKS_FWD : (is_adj<MODE>() ? IPT_MIN_BLOCKS_ADJ : IPT_MIN_BLOCKS_GRAPH));
 }
-// IPT_BVH_SERVER=1: BVH instances run 4 path waves + 1 traversal-server
-// wave per workgroup (ray compaction through an LDS queue, see trace_kernel).
-// Exact like the default, but measured SLOWER on the sphere scene (C2 size:
-// 21.0 vs 13.3 ms forward, profiles/r01_bvh_server.log): the traversal is
-// latency-bound (about 13 dependent node/leaf steps for the rays that reach
-// the tree), and funnelling every block's rays through one wave serialises
-// those chains behind two extra barriers per cast, while the VALU slots it
-// frees were not the bottleneck.  Off by default.
-#ifndef IPT_BVH_SERVER
-#define IPT_BVH_SERVER 0
-#endif
-// IPT_ADJ_WAVE_SWEEP=1: the adjoint's backward sweeps run as (path, vertex)
-// tasks spread over the whole wave (see trace_kernel); 0: each finishing lane
-// sweeps its own path.
-#ifndef IPT_ADJ_WAVE_SWEEP
-#define IPT_ADJ_WAVE_SWEEP 1
-#endif
+// Rejected and removed (round 3; the A/B logs under profiles/ keep the
+// evidence): a traversal-server wave per workgroup fed through an LDS ray
+// queue (r01_bvh_server.log: 21.0 vs 13.3 ms), the one-lane-per-ray binary
+// traversal (r01_variants_coop_notrav.log), the per-lane backward sweep
+// (r02_variants_adj_knobs_final.log: 7% slower), recorded prefix throughputs
+// (r02_variants_adj_sweep.log), quantised wide nodes (r02_variants_qnodes.log),
+// the forward's camera-ray ring (r02_variants_occupancy_after_cull.log), the
+// shadow target tested with its pair partner (r02_variants_shadow_target_pair.log)
+// and the tolerance-mode fast cast (r02_variants_fastcast.log: fails the
+// 1e-3 gradient bar).
 // Graph bins stay in LDS up to this size (KB), else global fp64 atomics.
 #ifndef IPT_GRAPH_LDS_KB
 #define IPT_GRAPH_LDS_KB 64
 #endif
 // IPT_RAY_RING=1: camera rays come from a per-wave LDS ring filled 64 at a
 // time (trace_kernel).  Brute-force adjoint only: C2 adjoint 3.01 -> 2.95 ms,
-// C3 3.93 -> 3.87 (profiles/r01_variants_ray_ring.log); the forward measured
-// no change (and spills 20 B more with it); the BVH instances' LDS is spoken
-// for; the graph also needs the target pixel.
+// C3 3.93 -> 3.87 (profiles/r01_variants_ray_ring.log); the BVH instances'
+// LDS is spoken for; the graph also needs the target pixel.
 #ifndef IPT_RAY_RING
 #define IPT_RAY_RING 1
 #endif
-#ifndef IPT_RAY_RING_FWD
-#define IPT_RAY_RING_FWD 0
-#endif
-// trace_kernel re-reads its TraceArgs from the kernarg segment each loop
-// iteration (see the loop head).  Offset: the ten scene pointers before it.
-#ifndef IPT_ARGS_RELOAD
-#define IPT_ARGS_RELOAD 1
-#endif
-[[maybe_unused]] constexpr size_t kTraceArgsOffset = 10 * sizeof(void *);
 constexpr int kRingFields = 9;  // d.xyz, XORWOW d, v0..v4
 template <int MODE, bool BVH>
 constexpr bool ring_on() {
-  return IPT_RAY_RING && !BVH && (MODE == 1 || (IPT_RAY_RING_FWD && MODE == 0));
+  return IPT_RAY_RING && !BVH && MODE == 1;
 }
-// Work enumeration of the adjoint and graph integrators.  Sample-major (1):
-// a wave's 64 lanes trace 64 different pixels, so their paths diverge at once
-// -- the LDS atomics of a vertex step hit different bins and few lanes of a
-// wave need the BVH tree in the same step; pixel-major (0): 64 samples of one
-// pixel, whose first vertices land on the same triangle (same bin).
-#ifndef IPT_ADJ_SAMPLE_MAJOR
-#define IPT_ADJ_SAMPLE_MAJOR 1
-#endif
-#ifndef IPT_GRAPH_SAMPLE_MAJOR
-#define IPT_GRAPH_SAMPLE_MAJOR 1
-#endif
-// IPT_BVH_COOP=1 (default): the BVH instances traverse with 8-lane groups
-// over 8-wide nodes (ipt_device.h::coop_cast); 0: one lane per ray over the
-// binary tree (closest_hit_bvh).
-#ifndef IPT_BVH_COOP
-#define IPT_BVH_COOP 1
-#endif
-constexpr bool kCoop = IPT_BVH_COOP && !IPT_BVH_SERVER;
-constexpr int kBlockSrv = kBlock + 64;
-template <bool BVH>
-constexpr int block_threads() {
-  return (BVH && IPT_BVH_SERVER) ? kBlockSrv : kBlock;
-}
-#define IPT_TRACE_BOUNDS __attribute__((amdgpu_flat_work_group_size(1, block_threads<BVH>()), amdgpu_waves_per_eu(min_blocks<MODE, BVH>() ? min_blocks<MODE, BVH>() : 1)))
+// Work enumeration of the adjoint and graph integrators: sample-major -- a
+// wave's 64 lanes trace 64 different pixels, so their paths diverge at once:
+// the LDS atomics of a vertex step hit different bins and few lanes of a wave
+// need the BVH tree in the same step (pixel-major: 64 samples of one pixel,
+// whose first vertices land on the same triangle, C2 adjoint 3.29 -> 3.24 ms,
+// sphere 23.8 -> 16.3 ms, profiles/r01_variants_adj_sample_major.log).
+#define IPT_TRACE_BOUNDS __attribute__((amdgpu_flat_work_group_size(1, kBlock), amdgpu_waves_per_eu(min_blocks<MODE, BVH>() ? min_blocks<MODE, BVH>() : 1)))
 // Profiling-only build (make variant DEFS=-DIPT_PHASE_TIMING): each wave
 // accumulates s_memtime cycles per phase of the loop; read with
 // ipt_debug_phase_cycles (tools/phase_timing.py).
@@ -410,94 +368,22 @@ __device__ unsigned long long g_phase_cycles[8];
 #define PHASE(i)
 #endif
 
-#ifndef IPT_SMALL_UNROLL
-#define IPT_SMALL_UNROLL 1
-#endif
-__device__ __forceinline__ int cast_bf(const TriIsect *__restrict__ isect, const TriPair *__restrict__ pairs,
-                                    const f2 *e3, int nT, V3 p, V3 d, float &t) {
-#if IPT_PAIRS
-#if IPT_SMALL_UNROLL
+// Path ray of the brute-force scenes: the unrolled pair loop with plane
+// offsets from LDS (nT <= 2 * kSmallPairs), else the packed pair loop.
+__device__ __forceinline__ int cast_bf(const TriPair *__restrict__ pairs, const f2 *e3, int nT, V3 p, V3 d, float &t) {
   if (e3) return closest_hit_pairs_small(pairs, e3, nT, p, d, t);
-#endif
   return closest_hit_pairs(pairs, nT, p, d, t);
-#else
-  return closest_hit(isect, nT, p, d, t);
-#endif
-}
-
-// Closest hit of a path ray (target < 0) or of a shadow ray towards emitter
-// triangle `target` (only `result == target` and then t are used): the
-// brute-force loop for small scenes, the BVH for large ones.
-template <bool BVH>
-__device__ __forceinline__ int cast(const TriIsect *__restrict__ isect, const TriPair *__restrict__ pairs,
-                                    const f2 *e3, int nT, const BvhView &bv, V3 p, V3 d, float &t, int target) {
-  if (BVH) {
-    if (target >= 0) return closest_hit_bvh<true>(bv, p, d, t, target);
-    return closest_hit_bvh<false>(bv, p, d, t);
-  }
-  return cast_bf(isect, pairs, e3, nT, p, d, t);
-}
-
-// ---- BVH ray compaction (the north_star's "wavefront ballot/prefix for ray
-// compaction").  In a BVH scene each path wave casts its rays through the
-// large-triangle pre-pass and the root test itself; the few rays that do
-// reach the tree (typically ~10% of lanes, spread over every wave) are
-// appended, by ballot + mbcnt prefix, to the workgroup's LDS queue, and ONE
-// server wave traverses them densely -- 64 rays per pass instead of four
-// waves each running the traversal loop for a handful of lanes.  Queue:
-// [field][slot], field = p.xyz, d.xyz, bt, bi; slot = 64 * path wave + rank.
-constexpr int kQFields = 8;
-constexpr int kQSlots = kBlock;
-__device__ __forceinline__ void srv_put(float *q, int slot, V3 p, V3 d, float bt, int bi) {
-  q[0 * kQSlots + slot] = p.x;
-  q[1 * kQSlots + slot] = p.y;
-  q[2 * kQSlots + slot] = p.z;
-  q[3 * kQSlots + slot] = d.x;
-  q[4 * kQSlots + slot] = d.y;
-  q[5 * kQSlots + slot] = d.z;
-  q[6 * kQSlots + slot] = bt;
-  q[7 * kQSlots + slot] = __int_as_float(bi);
-}
-__device__ __forceinline__ int lane_rank(uint64_t m) {
-  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-// Server wave: traverse every queued ray (counts[w] entries of path wave w),
-// 64 per pass, and write (bt, bi) back.  A shadow entry's initial bi is its
-// target (the pre-pass found it unoccluded so far).
-template <bool SHADOW>
-__device__ __forceinline__ void srv_serve(const BvhView &B, float *q, const int *counts, int lane) {
-  const int c0 = counts[0], c1 = counts[1], c2 = counts[2], c3 = counts[3];
-  const int n = c0 + c1 + c2 + c3;
-  for (int base = 0; base < n; base += 64) {
-    const int g = base + lane;
-    if (g < n) {
-      int slot;
-      if (g < c0) slot = g;
-      else if (g < c0 + c1) slot = 64 + (g - c0);
-      else if (g < c0 + c1 + c2) slot = 128 + (g - c0 - c1);
-      else slot = 192 + (g - c0 - c1 - c2);
-      const V3 p = mk(q[0 * kQSlots + slot], q[1 * kQSlots + slot], q[2 * kQSlots + slot]);
-      const V3 d = mk(q[3 * kQSlots + slot], q[4 * kQSlots + slot], q[5 * kQSlots + slot]);
-      float bt = q[6 * kQSlots + slot];
-      int bi = __float_as_int(q[7 * kQSlots + slot]);
-      bvh_traverse<SHADOW, 64>(B, p, d, bt, bi, bi);
-      q[6 * kQSlots + slot] = bt;
-      q[7 * kQSlots + slot] = __int_as_float(bi);
-    }
-  }
 }
 
 // Entry i of the small-scene LDS table (kE3Floats per pair): the three
-// edge-plane offsets of the pair as (A, B) float pairs, and in the fast-cast
-// build cn = -(c.n) of both triangles.
+// edge-plane offsets of the pair as (A, B) float pairs.
 __device__ __forceinline__ float small_table_entry(const TriPair *__restrict__ pairs, int i) {
   const int j = i / kE3Floats, k = i % kE3Floats, h = k & 1;
-  if (k < 6) return pairs[j].f[9 + 4 * (k >> 1)][h];
-  const TriPair &T = pairs[j];
-  return -fmaf(T.f[2][h], T.f[5][h], fmaf(T.f[1][h], T.f[4][h], T.f[0][h] * T.f[3][h]));
+  return pairs[j].f[9 + 4 * (k >> 1)][h];
 }
 
-// LDS carve-out of the BVH instances: node copy (16-B aligned) + stack.
+// LDS carve-out of the BVH instances (16-B aligned): wide nodes, large-pair
+// copies, emitter records, group stacks.
 __host__ __device__ inline size_t bvh_lds_offset(size_t base) { return (base + 15) & ~(size_t)15; }
 // Bytes of the culled path pre-pass's LDS copy of the large pairs (16-B
 // aligned, 36 floats per pair) and their original indices (2 ints per pair).
@@ -523,14 +409,15 @@ __device__ __forceinline__ float *big_lds_copy(const TraceArgs &a, float *at, fl
   return at + big_lds_bytes(a.bvh_nbig) / sizeof(float);
 }
 
+// TraceArgs is the kernel's FIRST parameter, so it sits at offset 0 of the
+// kernarg segment -- the in-loop reload below depends on that (IPT_ARGS_RELOAD).
 template <int MODE, bool SPEC, bool BVH>
 __global__ IPT_TRACE_BOUNDS void trace_kernel(
-    const TriIsect *__restrict__ isect, const TriPair *__restrict__ pairs, const TriGeom *__restrict__ geom,
-    const TriMat *__restrict__ mat, const BvhNode *__restrict__ bnodes, const BvhPair *__restrict__ bpairs,
-    const float *__restrict__ kd, const int *__restrict__ emit_tri, const float *__restrict__ emit_cdf,
-    const float *__restrict__ emit_pmf, const TraceArgs a, float *__restrict__ out_samples,
-    const float *__restrict__ adj, double *__restrict__ grad, const uint8_t *__restrict__ target,
-    double *__restrict__ edges) {
+    const TraceArgs a, const TriIsect *__restrict__ isect, const TriPair *__restrict__ pairs,
+    const TriGeom *__restrict__ geom, const TriMat *__restrict__ mat, const float *__restrict__ kd,
+    const int *__restrict__ emit_tri, const float *__restrict__ emit_cdf, const float *__restrict__ emit_pmf,
+    float *__restrict__ out_samples, const float *__restrict__ adj, double *__restrict__ grad,
+    const uint8_t *__restrict__ target, double *__restrict__ edges) {
   extern __shared__ double lds[];
   const int tid = threadIdx.x;
   // scene batch: this workgroup's material set and its place among the set's blocks
@@ -547,8 +434,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     }
   }
   const float *kdpi_g = a.kdpi_g ? a.kdpi_g + (size_t)set * 3 * a.nT : nullptr;
-  constexpr bool SERVE = BVH && IPT_BVH_SERVER;  // + a traversal-server wave
-  constexpr int nthr = block_threads<BVH>();
+  constexpr int nthr = kBlock;
   const int nT = a.nT, nE = a.nE;
   const int vmax = a.rec_cap;  // ADJ record capacity per lane (ADJU: ring slots)
   // LDS: [fp64 accumulators][kd table][kd/pi table][ADJ vertex records]
@@ -624,11 +510,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     ring = lds_rec + rec_words + (size_t)(tid >> 6) * (kRingFields * 64 + 4);
   }
   BvhView bv;
-  bv.nodes = bnodes;
-  bv.pairs = bpairs;
   bv.isect = isect;
-  bv.lnodes = nullptr;
-  bv.stack = nullptr;
   bv.big = nullptr;
   bv.big_idx = nullptr;
   bv.big_e3 = nullptr;
@@ -643,21 +525,13 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   cv.stk = nullptr;
   cv.stride = a.coop_stride;
   for (int k = 0; k < 6; ++k) cv.root[k] = a.root_box[k];
-  float *srvq = nullptr;  // SERVE: ray queue [kQFields][kQSlots]
-  int *srvc = nullptr;    // SERVE: per path wave queued count [4], live flag [4]
   if (BVH) {
     const size_t rec_words = is_adj<MODE>() ? (size_t)vmax * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock : 0;
     char *base = reinterpret_cast<char *>(lds);
     const size_t off = bvh_lds_offset((size_t)(reinterpret_cast<char *>(lds_rec + rec_words) - base));
-    float4 *ln = reinterpret_cast<float4 *>(base + off);
-    if (a.bvh_lds_nodes > 0) {
-      const float4 *g = reinterpret_cast<const float4 *>(bnodes);
-      for (int i = tid; i < 4 * a.bvh_lds_nodes; i += nthr) ln[i] = g[i];
-      bv.lnodes = ln;
-    }
-    float4 *lw = ln + 4 * a.bvh_lds_nodes;
+    float4 *lw = reinterpret_cast<float4 *>(base + off);
     cv.wn = a.bvh_wide;
-    if (kCoop && a.bvh_wide_lds > 0) {
+    if (a.bvh_wide_lds > 0) {
       for (int i = tid; i < kWideF4 * a.bvh_wide_lds; i += nthr) lw[i] = a.bvh_wide[i];
       cv.wn = lw;
       cv.wn_lds = true;
@@ -678,15 +552,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       bv.emit_is = after;
       after += 20 * nE;
     }
-    if (SERVE) {
-      srvq = after;
-      srvc = reinterpret_cast<int *>(srvq + kQFields * kQSlots);
-      bv.stack = reinterpret_cast<uint32_t *>(srvc + 8) + (tid >= kBlock ? tid - kBlock : 0);  // stride 64
-    } else if (kCoop) {
-      cv.stk = reinterpret_cast<uint32_t *>(after) + (tid >> 6) * 8 * a.coop_stride;
-    } else {
-      bv.stack = reinterpret_cast<uint32_t *>(after) + tid;
-    }
+    cv.stk = reinterpret_cast<uint32_t *>(after) + (tid >> 6) * 8 * a.coop_stride;
   }
   for (int i = tid; i < n_acc; i += nthr) lds_acc[i] = 0.0;
   __syncthreads();
@@ -706,7 +572,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     }
   };
 
-  if (!SERVE || tid < kBlock) {  // path waves
+  {  // the wave's persistent loop
   // wave-uniform sample range (static partition, regenerated per lane)
   const uint32_t wave = __builtin_amdgcn_readfirstlane((sblock * kBlock + tid) >> 6);
   const uint32_t nwaves = (sgrid * kBlock) >> 6;
@@ -763,7 +629,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   int ring_n = 0, ring_h = 0;  // slots left, next slot
   const int lane = tid & 63;
   for (;;) {
-#if IPT_ARGS_RELOAD && defined(__HIP_DEVICE_COMPILE__)  // (the host pass has no AS4 copy)
+#if defined(__HIP_DEVICE_COMPILE__)  // (the host pass has no AS4 copy)
     // The launch arguments, re-read from the kernarg segment every iteration
     // through a pointer the compiler cannot see through: left alone it keeps
     // the loop-invariant fields (camera, divisors, pointers) in SGPRs for
@@ -771,8 +637,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     // a v_readlane (a VALU instruction) at every use.  Scalar loads hit the
     // constant cache.  This `a` shadows the parameter inside the loop.
     typedef __attribute__((address_space(4))) const TraceArgs cst_args;
-    const cst_args *apc = (const cst_args *)((__attribute__((address_space(4))) const char *)
-                                                 __builtin_amdgcn_kernarg_segment_ptr() + kTraceArgsOffset);
+    const cst_args *apc = (const cst_args *)__builtin_amdgcn_kernarg_segment_ptr();  // first parameter: offset 0
     asm volatile("" : "+s"(apc));
     const TraceArgs a = *apc;
 #endif
@@ -876,7 +741,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       next += (uint64_t)__popcll(need);
     }
     PHASE(0)
-    if (!SERVE && __ballot(active) == 0) break;
+    if (__ballot(active) == 0) break;
 #ifdef IPT_PHASE_TIMING
     tacc[6] += 1;
     tacc[7] += __popcll(__ballot(active));
@@ -885,29 +750,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     // ================= phase 1: path ray (radiance, path_trace.cu:111-144)
     float t = 0.f;
     int hit = -1;
-    if (SERVE) {  // pre-pass + root test here; the tree part via the server wave
-      const int wl = tid >> 6;
-      bool qn = false;
-      if (active) {
-        bvh_prepass<false>(bv, p, d, t, hit, -1);
-        qn = bvh_root_test(bv, p, d, t);
-      }
-      const uint64_t qm = __ballot(qn);
-      const int slot = 64 * wl + lane_rank(qm);
-      if (qn) srv_put(srvq, slot, p, d, t, hit);
-      const bool live = __ballot(active) != 0;
-      if ((tid & 63) == 0) {
-        srvc[wl] = (int)__popcll(qm);
-        srvc[4 + wl] = live ? 1 : 0;
-      }
-      __syncthreads();  // B: queue + liveness published
-      if (!(srvc[4] | srvc[5] | srvc[6] | srvc[7])) break;  // the whole workgroup is done
-      __syncthreads();  // C: the server has traversed the queue
-      if (qn) {
-        t = srvq[6 * kQSlots + slot];
-        hit = __float_as_int(srvq[7 * kQSlots + slot]);
-      }
-    } else if (BVH && kCoop) {  // pre-pass per lane, the tree part by 8-lane groups
+    if (BVH) {  // pre-pass per lane, the tree part by 8-lane groups
       bool qn = false;
       if (active) {
         bvh_prepass<false>(bv, p, d, t, hit, -1);
@@ -915,10 +758,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       }
       coop_cast<false>(cv, qn, p, d, t, hit);
     } else if (active) {
-      if (!BVH && IPT_PATH_CULL && e3)
+      if (IPT_PATH_CULL && e3)
         hit = closest_hit_pairs_culled((const lds_f32 *)lds_pr, a.pboxes, nT, p, d, t);
       else
-        hit = cast<BVH>(isect, pairs, e3, nT, bv, p, d, t, -1);
+        hit = cast_bf(pairs, e3, nT, p, d, t);
     }
     PHASE(1)
     const bool vertex = active && hit >= 0;
@@ -1022,35 +865,19 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     float ts = 0.f;
     int hs = -1;
     const int et = shadow ? emit_tri[emitter] : -1;
-    if (SERVE) {  // same split as the path ray, with the shadow early-out
-      const int wl = tid >> 6;
-      bool qn = false;
-      if (shadow && bvh_prepass<true>(bv, p, sd, ts, hs, et)) qn = bvh_root_test(bv, p, sd, ts);
-      const uint64_t qm = __ballot(qn);
-      const int slot = 64 * wl + lane_rank(qm);
-      if (qn) srv_put(srvq, slot, p, sd, ts, hs);
-      if ((tid & 63) == 0) srvc[wl] = (int)__popcll(qm);
-      __syncthreads();  // D: shadow queue published
-      __syncthreads();  // E: the server has traversed it
-      if (qn) {
-        ts = srvq[6 * kQSlots + slot];
-        hs = __float_as_int(srvq[7 * kQSlots + slot]);
-      }
-    }
     if (__ballot(shadow)) {
-      if (BVH && kCoop) {
+      if (BVH) {
         bool qn = false;
         if (shadow && bvh_prepass<true>(bv, p, sd, ts, hs, et,
                                         a.big_pomask ? a.big_pomask[tri * nE + emitter] : 0xffffffffu, emitter))
           qn = coop_root_test(cv, p, sd, ts);
         coop_cast<true>(cv, qn, p, sd, ts, hs);
-      } else if (!SERVE && shadow) {
-        if (!BVH && IPT_SHADOW_CULL && e3)
+      } else if (shadow) {
+        if (IPT_SHADOW_CULL && e3)
           hs = shadow_hit_pairs_small((const lds_f32 *)lds_is, pairs, a.pboxes, e3, nT, p, sd, et, ts,
-                                      po ? ((const lds_u32c *)lds_po)[tri * nE + emitter] : 0xffffffffu,
-                                      IPT_PATH_CULL && IPT_SHADOW_TARGET_PAIR ? (const lds_f32 *)lds_pr : nullptr);
+                                      po ? ((const lds_u32c *)lds_po)[tri * nE + emitter] : 0xffffffffu);
         else
-          hs = cast<BVH>(isect, pairs, e3, nT, bv, p, sd, ts, et);
+          hs = cast_bf(pairs, e3, nT, p, sd, ts);
       }
       PHASE(3)
       if (shadow && hs == et) {  // must hit the sampled emitter itself
@@ -1115,11 +942,6 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         rec[0] = __uint_as_float((uint32_t)tri | ((uint32_t)emit_et << 16));
         rec[fs] = emit_s;
         rec[2 * fs] = coeff;
-        if (IPT_ADJ_STORE_M) {  // M_k: the throughput before this vertex's update
-          rec[kRecM * fs] = M.x;
-          rec[(kRecM + 1) * fs] = M.y;
-          rec[(kRecM + 2) * fs] = M.z;
-        }
         if (SPEC) {
           rec[kRecSD * fs] = specd;
           rec[(kRecSD + 1) * fs] = speci;
@@ -1277,104 +1099,20 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           rhi = lo;
           active = true;
         }
-      } else if (MODE == MODE_ADJ && !IPT_ADJ_WAVE_SWEEP) {
-        // backward sweep over the recorded vertices (oracle adjoint_sample)
-        const int K = k;
-#ifdef IPT_ABL_NOSWEEP  // timing-only ablation build: no backward sweep (no gradients)
-        if (0) {
-#else
-        if (K > 0) {
-#endif
-          const size_t fs = (size_t)vmax * kBlock;
-          const uint64_t pixel = item_pixel(a, witem);
-          const float ax = adj[pixel * 3 + 0] / (float)a.spp;
-          const float ay = adj[pixel * 3 + 1] / (float)a.spp;
-          const float az = adj[pixel * 3 + 2] / (float)a.spp;
-          V3 S = mk(0.f, 0.f, 0.f);
-          // T_j = kd/pi (+ Ks*speci), D_j = kd (+ Ks*specd): exactly the forward's values
-          auto rec_lo = [&](int et, float es) {  // the forward's lo, same products
-            const TriMat &me = mat[et];
-            return mk(me.ke[0] * es, me.ke[1] * es, me.ke[2] * es);
-          };
-          auto tdiff = [&](int tj, float si, float &x, float &y, float &z) {
-            const V3 tp = kdpi3(tj);
-            x = tp.x; y = tp.y; z = tp.z;
-            if (SPEC) {
-              const TriMat &mj = mat[tj];
-              x = x + mj.ks[0] * si; y = y + mj.ks[1] * si; z = z + mj.ks[2] * si;
-            }
-          };
-          auto ddir = [&](int tj, float sdj, float &x, float &y, float &z) {
-            const V3 kt = kd3(tj);
-            x = kt.x; y = kt.y; z = kt.z;
-            if (SPEC) {
-              const TriMat &mj = mat[tj];
-              x = x + mj.ks[0] * sdj; y = y + mj.ks[1] * sdj; z = z + mj.ks[2] * sdj;
-            }
-          };
-          if (escaped) {
-            const float *r = lds_rec + (size_t)(K - 1) * kBlock + tid;
-            float dx, dy, dz;
-            const uint32_t f0 = __float_as_uint(r[0]);
-            const V3 lk = rec_lo((int)(f0 >> 16), r[fs]);
-            ddir((int)(f0 & 0xffffu), SPEC ? r[kRecSD * fs] : 0.f, dx, dy, dz);
-            S = mk(Le.x + dx * lk.x, Le.y + dy * lk.y, Le.z + dz * lk.z);
-          }
-          for (int kk = K - 1; kk >= 0; --kk) {
-            // prefix throughput M_kk: recorded by the forward, or recomputed
-            // with exactly the forward's operations
-            const float *r = lds_rec + (size_t)kk * kBlock + tid;
-            V3 Mk = mk(1.f, 1.f, 1.f);
-            if (IPT_ADJ_STORE_M) {
-              Mk = mk(r[kRecM * fs], r[(kRecM + 1) * fs], r[(kRecM + 2) * fs]);
-            } else {
-#ifdef IPT_ABL_NOPREFIX  // timing-only ablation build: no prefix recompute (wrong gradients)
-              if (0)
-#endif
-              for (int j = 0; j < kk; ++j) {
-                const float *rj = lds_rec + (size_t)j * kBlock + tid;
-                const float cj = rj[2 * fs];
-                float tx, ty, tz;
-                tdiff((int)(__float_as_uint(rj[0]) & 0xffffu), SPEC ? rj[(kRecSD + 1) * fs] : 0.f, tx, ty, tz);
-                Mk = mk((Mk.x * tx) * cj, (Mk.y * ty) * cj, (Mk.z * tz) * cj);
-              }
-            }
-            const uint32_t f0 = __float_as_uint(r[0]);
-            const int tk = (int)(f0 & 0xffffu);
-            const V3 lk = rec_lo((int)(f0 >> 16), r[fs]);
-            const float ck = r[2 * fs], sdk = SPEC ? r[kRecSD * fs] : 0.f, si = SPEC ? r[(kRecSD + 1) * fs] : 0.f;
-            const bool last_esc = escaped && kk == K - 1;
-            const bool continued = (kk < K - 1) || escaped;
-            V3 dLd = Mk;
-            if (last_esc) dLd = mk(dLd.x + M.x, dLd.y + M.y, dLd.z + M.z);
-            V3 gk = mk(dLd.x * lk.x, dLd.y * lk.y, dLd.z * lk.z);
-            if (continued) {
-              const float cpi = ck / kPiF;
-              gk = mk(gk.x + (cpi * Mk.x) * S.x, gk.y + (cpi * Mk.y) * S.y, gk.z + (cpi * Mk.z) * S.z);
-            }
-            {
-              const int sl = a.grad_map ? a.grad_map[tk] : tk;
-              const double v[3] = {(double)(ax * gk.x), (double)(ay * gk.y), (double)(az * gk.z)};
-              bins_add(sl >= 0, grad, sl >= 0 ? (size_t)sl * 3 : (size_t)tk * 3, 3, v);
-            }
-            float dx, dy, dz, tx, ty, tz;
-            ddir(tk, sdk, dx, dy, dz);
-            tdiff(tk, si, tx, ty, tz);
-            S = mk((Le.x + dx * lk.x) + (tx * ck) * S.x, (Le.y + dy * lk.y) + (ty * ck) * S.y,
-                   (Le.z + dz * lk.z) + (tz * ck) * S.z);
-          }
-        }
       }
     }
-    if (MODE == MODE_ADJ && IPT_ADJ_WAVE_SWEEP) {
-      // Wave-parallel sweep.  The vertices of the paths that finished in this
-      // iteration become tasks (path, vertex kk) spread over all 64 lanes:
-      // task kk recomputes its prefix throughput M_kk from records 0..kk-1
-      // and its suffix S_kk+1 from records kk+1..K-1 of the owner's LDS
-      // column with exactly the per-lane sweep's operations (the same floats;
-      // only the order of the fp64 gradient atomics changes), then adds its
-      // contribution.  The per-lane sweep ran on the ~1/3 of lanes whose path
-      // just ended while the rest idled.
+    if (MODE == MODE_ADJ) {
+      // Wave-parallel backward sweep (oracle adjoint_sample).  The vertices of
+      // the paths that finished in this iteration become tasks (path, vertex
+      // kk), packed into rounds of <= 64 consecutive lanes without splitting a
+      // path (K <= rec_cap <= 63).  Each task lane reads ITS vertex's record
+      // once; the prefix throughputs M_kk then pass left to right and the
+      // suffixes S_kk+1 right to left between neighbouring lanes (wave shifts),
+      // every step with the forward's / the per-path sweep's own operations,
+      // so each M_kk and S_kk+1 is the same float as in the oracle's single
+      // sweep (only the order of the fp64 gradient atomics changes).  Round 2
+      // recomputed both chains per task from the owner's LDS column (O(K^2)
+      // record reads, loops as long as the wave's longest chain).
       const int Kf = (finished && k > 0) ? k : 0;
 #ifdef IPT_ABL_NOWSWEEP  // timing-only ablation build: no backward sweep (no gradients)
       if (0) {
@@ -1402,83 +1140,63 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           }
         }
         const size_t fs = (size_t)vmax * kBlock;
-        for (int base = 0; base < T; base += 64) {
+        int base = 0;
+        while (base < T) {  // wave-uniform
+          // this round: the whole paths whose tasks end by base + 64
+          const uint64_t fit = __ballot(Kf > 0 && inc <= base + 64);
+          const int next = __shfl(inc, 63 - (int)__builtin_clzll(fit));
           const int t = base + lane;
+          const bool valid = t < next;
           int ow = 0;  // owner lane: the smallest with inc > t
           for (int step = 32; step >= 1; step >>= 1)
             if (__shfl(inc, ow + step - 1) <= t) ow += step;
+          // every shuffle reads a lane that may not hold a task of this
+          // round, so all of them run with the whole wave active (a
+          // ds_bpermute from an inactive lane returns 0)
           const int KL = __shfl(Kf, ow);
-          const int kk = t - (__shfl(inc, ow) - KL);
+          const int inco = __shfl(inc, ow);
+          const int kk = valid ? t - (inco - KL) : 0;
+          const int rr = valid ? KL - 1 - kk : 0;  // vertices after this one
           const bool esc = __shfl(escaped ? 1 : 0, ow) != 0;
           const float ax = __shfl(wx, ow), ay = __shfl(wy, ow), az = __shfl(wz, ow);
           const V3 LeL = mk(__shfl(Le.x, ow), __shfl(Le.y, ow), __shfl(Le.z, ow));
           const V3 ML = mk(__shfl(M.x, ow), __shfl(M.y, ow), __shfl(M.z, ow));
-          if (t < T) {
-            const float *col = lds_rec + (tid & ~63) + ow;  // the owner's record column
-            auto rec_lo = [&](uint32_t f0, float es) {  // the forward's lo, same products
-              const TriMat &me = mat[f0 >> 16];
-              return mk(me.ke[0] * es, me.ke[1] * es, me.ke[2] * es);
-            };
-            auto tdiff = [&](int tj, const float *r) {  // T_j = kd/pi (+ Ks*speci)
-              V3 x = kdpi3(tj);
-              if (SPEC) {
-                const TriMat &mj = mat[tj];
-                const float si = r[(kRecSD + 1) * fs];
-                x = mk(x.x + mj.ks[0] * si, x.y + mj.ks[1] * si, x.z + mj.ks[2] * si);
-              }
-              return x;
-            };
-            auto ddir = [&](int tj, const float *r) {  // D_j = kd (+ Ks*specd)
-              V3 x = kd3(tj);
-              if (SPEC) {
-                const TriMat &mj = mat[tj];
-                const float sd = r[kRecSD * fs];
-                x = mk(x.x + mj.ks[0] * sd, x.y + mj.ks[1] * sd, x.z + mj.ks[2] * sd);
-              }
-              return x;
-            };
-            // suffix S_kk+1, built from the end exactly like the per-lane sweep
-            V3 S = mk(0.f, 0.f, 0.f);
-            if (esc) {
-              const float *r = col + (size_t)(KL - 1) * kBlock;
-              const uint32_t f0 = __float_as_uint(r[0]);
-              const V3 lk = rec_lo(f0, r[fs]);
-              const V3 dj = ddir((int)(f0 & 0xffffu), r);
-              S = mk(LeL.x + dj.x * lk.x, LeL.y + dj.y * lk.y, LeL.z + dj.z * lk.z);
-            }
-            for (int j = KL - 1; j > kk; --j) {
-              const float *r = col + (size_t)j * kBlock;
-              const uint32_t f0 = __float_as_uint(r[0]);
-              const int tj = (int)(f0 & 0xffffu);
-              const V3 lk = rec_lo(f0, r[fs]);
-              const float cj = r[2 * fs];
-              const V3 dj = ddir(tj, r), tjv = tdiff(tj, r);
-              S = mk((LeL.x + dj.x * lk.x) + (tjv.x * cj) * S.x, (LeL.y + dj.y * lk.y) + (tjv.y * cj) * S.y,
-                     (LeL.z + dj.z * lk.z) + (tjv.z * cj) * S.z);
-            }
-            // prefix throughput M_kk: recorded by the forward (IPT_ADJ_STORE_M) or
-            // recomputed with exactly its operations
-            V3 Mk = mk(1.f, 1.f, 1.f);
-            if (IPT_ADJ_STORE_M) {
-              const float *r = col + (size_t)kk * kBlock;
-              Mk = mk(r[kRecM * fs], r[(kRecM + 1) * fs], r[(kRecM + 2) * fs]);
-            } else {
-              for (int j = 0; j < kk; ++j) {
-                const float *r = col + (size_t)j * kBlock;
-                const float cj = r[2 * fs];
-                const V3 tjv = tdiff((int)(__float_as_uint(r[0]) & 0xffffu), r);
-                Mk = mk((Mk.x * tjv.x) * cj, (Mk.y * tjv.y) * cj, (Mk.z * tjv.z) * cj);
-              }
-            }
-            const float *r = col + (size_t)kk * kBlock;
-            const uint32_t f0 = __float_as_uint(r[0]);
-            const int tk = (int)(f0 & 0xffffu);
-            const V3 lk = rec_lo(f0, r[fs]);
-            const float ck = r[2 * fs];
+          // this task's record (lanes past the round read vertex 0 of a valid column)
+          const float *r = lds_rec + (tid & ~63) + (valid ? ow : lane) + (size_t)kk * kBlock;
+          const uint32_t f0 = valid ? __float_as_uint(r[0]) : 0u;
+          const float es = r[fs], ck = r[2 * fs];
+          // (the min()s keep a mis-indexed record from reaching global memory out of bounds)
+          const int tk = min((int)(f0 & 0xffffu), nT - 1);
+          const TriMat &me = mat[min((int)(f0 >> 16), nT - 1)];
+          const V3 lk = mk(me.ke[0] * es, me.ke[1] * es, me.ke[2] * es);  // the forward's lo, same products
+          V3 dj = kd3(tk), tv = kdpi3(tk);  // D = kd (+ Ks*specd), T = kd/pi (+ Ks*speci)
+          if (SPEC) {
+            const TriMat &mj = mat[tk];
+            const float sdv = r[kRecSD * fs], si = r[(kRecSD + 1) * fs];
+            dj = mk(dj.x + mj.ks[0] * sdv, dj.y + mj.ks[1] * sdv, dj.z + mj.ks[2] * sdv);
+            tv = mk(tv.x + mj.ks[0] * si, tv.y + mj.ks[1] * si, tv.z + mj.ks[2] * si);
+          }
+          // prefix: M_0 = 1, M_s = (M_{s-1} * T_{s-1}) * c_{s-1} from the left neighbour
+          V3 Mk = mk(1.f, 1.f, 1.f);
+          for (int s = 1; __ballot(valid && kk >= s); ++s) {
+            const V3 N = mk((Mk.x * tv.x) * ck, (Mk.y * tv.y) * ck, (Mk.z * tv.z) * ck);
+            const V3 Nl = mk(wave_shr1(N.x), wave_shr1(N.y), wave_shr1(N.z));
+            if (kk == s) Mk = Nl;
+          }
+          // suffix: S_K = escaped ? Le + D_{K-1} lo_{K-1} : 0, S_j = (Le + D_j lo_j) + (T_j c_j) S_{j+1}
+          const V3 A = mk(LeL.x + dj.x * lk.x, LeL.y + dj.y * lk.y, LeL.z + dj.z * lk.z);
+          const V3 B = mk(tv.x * ck, tv.y * ck, tv.z * ck);
+          V3 S = (esc && rr == 0) ? A : mk(0.f, 0.f, 0.f);
+          for (int s = 1; __ballot(valid && rr >= s); ++s) {
+            const V3 H = mk(A.x + B.x * S.x, A.y + B.y * S.y, A.z + B.z * S.z);
+            const V3 Hr = mk(wave_shl1(H.x), wave_shl1(H.y), wave_shl1(H.z));
+            if (rr == s) S = Hr;
+          }
+          if (valid) {
             V3 dLd = Mk;
-            if (esc && kk == KL - 1) dLd = mk(dLd.x + ML.x, dLd.y + ML.y, dLd.z + ML.z);
+            if (esc && rr == 0) dLd = mk(dLd.x + ML.x, dLd.y + ML.y, dLd.z + ML.z);
             V3 gk = mk(dLd.x * lk.x, dLd.y * lk.y, dLd.z * lk.z);
-            if (kk < KL - 1 || esc) {
+            if (rr > 0 || esc) {
               const float cpi = ck / kPiF;
               gk = mk(gk.x + (cpi * Mk.x) * S.x, gk.y + (cpi * Mk.y) * S.y, gk.z + (cpi * Mk.z) * S.z);
             }
@@ -1490,6 +1208,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             bins_add(sl >= 0, grad, sl >= 0 ? (size_t)sl * 3 : (size_t)tk * 3, 3, v);
 #endif
           }
+          base = next;
         }
       }
     }
@@ -1500,17 +1219,6 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     for (int i = 0; i < 8; ++i) atomicAdd(&g_phase_cycles[i], (unsigned long long)tacc[i]);
 #endif
 
-  } else {  // traversal-server wave: mirrors the path waves' barriers B..E
-    const int lane = tid - kBlock;
-    for (;;) {
-      __syncthreads();  // B
-      if (!(srvc[4] | srvc[5] | srvc[6] | srvc[7])) break;
-      srv_serve<false>(bv, srvq, srvc, lane);
-      __syncthreads();  // C
-      __syncthreads();  // D
-      srv_serve<true>(bv, srvq, srvc, lane);
-      __syncthreads();  // E
-    }
   }
 
   if (MODE != MODE_FWD) {
@@ -1614,12 +1322,10 @@ struct GpuScene {
   float *emit_cdf = nullptr, *emit_pmf = nullptr;
   double *emit_pmfr = nullptr;  // TraceArgs::emit_pmfr
   bool has_ks = false;      // some material has a Phong lobe
-  BvhNode *bnodes = nullptr;
-  BvhPair *bpairs = nullptr;
   TriPair *big_pairs = nullptr;
   int32_t *big_idx = nullptr;
   PairBox2 *big_boxes = nullptr;
-  float4 *wide = nullptr;  // WideNode or QWideNode records (IPT_BVH_QNODES)
+  float4 *wide = nullptr;  // WideNode records
   TriIsect *wtris = nullptr;
   PairBox2 *pboxes = nullptr;  // pair acceptance boxes (small scenes' culled shadow casts)
   uint32_t *pomask = nullptr;  // shadow rays' potential occluders (small scenes)
@@ -1680,10 +1386,10 @@ GpuScene *gpu_upload(const HostScene &host, std::string *err) {
   pack_pairs(host.isect.data(), (int)host.isect.size(), pairs.data());
   if (upload(&s->isect, host.isect) || upload(&s->pairs, pairs) || upload(&s->geom, host.geom) || upload(&s->mat, host.mat) ||
       upload(&s->kd, host.kd) || upload(&s->emit_tri, host.emit_tri) || upload(&s->emit_cdf, host.emit_cdf) ||
-      upload(&s->emit_pmf, host.emit_pmf) || upload(&s->emit_pmfr, pmf_reciprocals(host.emit_pmf)) || upload(&s->bnodes, host.bvh_nodes) || upload(&s->bpairs, host.bvh_pairs) ||
+      upload(&s->emit_pmf, host.emit_pmf) || upload(&s->emit_pmfr, pmf_reciprocals(host.emit_pmf)) ||
       upload(&s->big_pairs, host.bvh_big_pairs) || upload(&s->big_idx, host.bvh_big_idx) ||
       upload(&s->big_boxes, host.bvh_big_boxes) ||
-      (IPT_BVH_QNODES ? upload_as_f4(&s->wide, host.bvh_qwide) : upload_as_f4(&s->wide, host.bvh_wide)) ||
+      upload_as_f4(&s->wide, host.bvh_wide) ||
       upload(&s->wtris, host.bvh_wtris) || upload(&s->pboxes, pair_boxes(host)) ||
       upload(&s->pomask, shadow_occluder_masks(host)) ||
       upload(&s->big_pomask, host.bvh_big_idx.empty()
@@ -1746,8 +1452,6 @@ void gpu_free(GpuScene *s) {
   (void)hipFree(s->emit_cdf);
   (void)hipFree(s->emit_pmf);
   (void)hipFree(s->emit_pmfr);
-  (void)hipFree(s->bnodes);
-  (void)hipFree(s->bpairs);
   (void)hipFree(s->big_pairs);
   (void)hipFree(s->big_idx);
   (void)hipFree(s->big_boxes);
@@ -1804,7 +1508,7 @@ static int resident_grid(GpuScene *s, size_t lds_bytes, int *grid) {
   const int slot = MODE * 4 + (SPEC ? 2 : 0) + (BVH ? 1 : 0);
   if (s->grid[slot] == 0 || s->grid_lds[slot] != lds_bytes) {
     int per_cu = 0, cus = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<MODE, SPEC, BVH>, block_threads<BVH>(),
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<MODE, SPEC, BVH>, kBlock,
                                                          lds_bytes));
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device));
     if (per_cu <= 0) {
@@ -1846,7 +1550,7 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.sample_major = 0;
   a.kdpi_g = nullptr;
   a.kd_tables = s->host.nT <= kMaxTableTris ? 1 : 0;
-  a.small_pairs = (IPT_PAIRS && IPT_SMALL_UNROLL && s->host.nT <= 2 * kSmallPairs) ? 1 : 0;
+  a.small_pairs = s->host.nT <= 2 * kSmallPairs ? 1 : 0;
   a.npix = (uint64_t)rows * p.width;
   a.row0 = p.row_begin;
   a.row_step = p.row_step > 1 ? p.row_step : 1;
@@ -1855,8 +1559,6 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.m_spp = p.spp > 1 ? ~0ull / (uint64_t)p.spp + 1 : 0;
   a.m_W = p.width > 1 ? ~0ull / (uint64_t)p.width + 1 : 0;
   a.m_npix = a.npix > 1 ? ~0ull / a.npix + 1 : 0;
-  a.bvh_lds_nodes = 0;
-  a.bvh_stack = 0;
   a.bvh_nbig = 0;
   a.bvh_big = nullptr;
   a.bvh_big_idx = nullptr;
@@ -1903,32 +1605,25 @@ static bool use_bvh(const GpuScene *s) {
   return s->host.nT >= kBvhMinTris;
 }
 
-// BVH LDS carve-out on top of `base` bytes; fills the args' BVH fields.
-// server: the megakernel's layout (ray queue + a 64-lane stack); else one
-// stack per thread of a 256-thread block (the closest-hit probe).
-static size_t bvh_lds(const GpuScene *s, TraceArgs &a, size_t base, bool server, bool stage = true,
-                      bool big_copy = true) {
-  const size_t nn = s->host.bvh_nodes.size();
-  a.bvh_lds_nodes = (stage && !kCoop && nn * sizeof(BvhNode) <= (size_t)kBvhLdsNodeBytes) ? (int)nn : 0;
+// BVH LDS carve-out on top of `base` bytes; fills the args' BVH fields:
+// [wide nodes if staged][large pairs' plane offsets][large pairs' copy if
+// taken][emitter records][the wave's 8 group stacks].
+static size_t bvh_lds(const GpuScene *s, TraceArgs &a, size_t base, bool stage = true, bool big_copy = true) {
   const size_t nw = s->host.bvh_wide.size();
   a.bvh_wide = s->wide;
   a.bvh_wtris = s->wtris;
-  a.bvh_wide_lds = (stage && kCoop && nw * kWideF4 * sizeof(float4) <= (size_t)kBvhLdsNodeBytes) ? (int)nw : 0;
+  a.bvh_wide_lds = (stage && nw * kWideF4 * sizeof(float4) <= (size_t)kBvhLdsNodeBytes) ? (int)nw : 0;
   a.bvh_big_lds = big_copy && IPT_PATH_CULL ? 1 : 0;
   a.big_pomask = (IPT_SHADOW_PO && s->host.nE > 0 && !s->host.bvh_big_idx.empty()) ? s->big_pomask : nullptr;
   a.coop_stride = 7 * s->host.bvh_wdepth + 8;
-  a.bvh_stack = std::max(1, s->host.bvh_depth);
   a.bvh_nbig = (int)s->host.bvh_big_pairs.size();
   a.bvh_big = s->big_pairs;
   a.bvh_big_idx = s->big_idx;
   a.bvh_big_boxes = s->big_boxes;
-  const size_t head = bvh_lds_offset(base) + (size_t)a.bvh_lds_nodes * sizeof(BvhNode) +
-                      (size_t)a.bvh_wide_lds * kWideF4 * sizeof(float4) + (size_t)a.bvh_nbig * 6 * sizeof(float) +
-                      (a.bvh_big_lds ? big_lds_bytes(a.bvh_nbig) : 0) + emit_lds_bytes(s->host.nE);
-  if (kCoop) return head + (size_t)(kBlock / 64) * 8 * a.coop_stride * sizeof(uint32_t);
-  if (server)
-    return head + (size_t)kQFields * kQSlots * sizeof(float) + 8 * sizeof(int) + (size_t)a.bvh_stack * 64 * sizeof(uint32_t);
-  return head + (size_t)a.bvh_stack * kBlock * sizeof(uint32_t);
+  const size_t head = bvh_lds_offset(base) + (size_t)a.bvh_wide_lds * kWideF4 * sizeof(float4) +
+                      (size_t)a.bvh_nbig * 6 * sizeof(float) + (a.bvh_big_lds ? big_lds_bytes(a.bvh_nbig) : 0) +
+                      emit_lds_bytes(s->host.nE);
+  return head + (size_t)(kBlock / 64) * 8 * a.coop_stride * sizeof(uint32_t);
 }
 
 static size_t table_bytes(const TraceArgs &a) {
@@ -1975,7 +1670,7 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
   StreamScratch ctr;
   b.chunk = 0;
   b.chunk_ctr = nullptr;
-  if (IPT_DYN_CHUNKS && !(BVH && IPT_BVH_SERVER)) {
+  if (IPT_DYN_CHUNKS) {
     // ~IPT_DYN_CHUNKS_PER_WAVE chunks per wave, a multiple of 64 items, 64..4096
     const uint64_t waves = (uint64_t)(a.nscenes > 1 ? b.bps : grid) * (kBlock / 64);
     uint64_t c = (a.n_samples / (waves * IPT_DYN_CHUNKS_PER_WAVE) + 63) / 64 * 64;
@@ -1986,9 +1681,9 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
     HIP_TRY(hipMemsetAsync(ctr.p, 0, bytes, st));
     b.chunk_ctr = (uint32_t *)ctr.p;
   }
-  hipLaunchKernelGGL((trace_kernel<MODE, SPEC, BVH>), dim3(grid), dim3(block_threads<BVH>()), lds, st, s->isect, s->pairs, s->geom,
-                     s->mat, s->bnodes, s->bpairs, kd_dev ? kd_dev : s->kd, s->emit_tri, s->emit_cdf, s->emit_pmf, b,
-                     out, adj, grad, target, edges);
+  hipLaunchKernelGGL((trace_kernel<MODE, SPEC, BVH>), dim3(grid), dim3(kBlock), lds, st, b, s->isect, s->pairs, s->geom,
+                     s->mat, kd_dev ? kd_dev : s->kd, s->emit_tri, s->emit_cdf, s->emit_pmf, out, adj, grad, target,
+                     edges);
   HIP_TRY(hipGetLastError());
   return 0;
 }
@@ -2019,11 +1714,11 @@ static int launch_bvh_pick(GpuScene *s, TraceArgs &a, size_t *lds) {
     int best = -1, best_per_cu = 0;
     for (int k = 0; k < 4; ++k) {
       TraceArgs b = a;
-      const size_t l = bvh_lds(s, b, base, IPT_BVH_SERVER != 0, opt[k][0], opt[k][1]);
+      const size_t l = bvh_lds(s, b, base, opt[k][0], opt[k][1]);
       if (l > 160 * 1024) continue;
       int per_cu = 0;
       HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<MODE, SPEC, true>,
-                                                           block_threads<true>(), l));
+                                                           kBlock, l));
       if (per_cu > best_per_cu) {
         best = k;
         best_per_cu = per_cu;
@@ -2037,7 +1732,7 @@ static int launch_bvh_pick(GpuScene *s, TraceArgs &a, size_t *lds) {
     s->pick_base[slot] = base;
   }
   const int k = s->pick_opt[slot];
-  *lds = bvh_lds(s, a, base, IPT_BVH_SERVER != 0, opt[k][0], opt[k][1]);
+  *lds = bvh_lds(s, a, base, opt[k][0], opt[k][1]);
   return 0;
 }
 
@@ -2139,7 +1834,7 @@ int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const f
     return -1;
   }
   TraceArgs a = make_args(s, p);
-  a.sample_major = IPT_ADJ_SAMPLE_MAJOR;
+  a.sample_major = 1;  // sample-major (see IPT_TRACE_BOUNDS)
   if (s->grad_map) {
     a.grad_slots = kLdsGradBytes / (3 * (int)sizeof(double));
     a.grad_map = s->grad_map;
@@ -2165,7 +1860,7 @@ int gpu_graph(GpuScene *s, const RenderParams &p, const uint8_t *target_dev, dou
   const size_t bins = graph_lds_doubles(s->host.nT, s->host.nE) * sizeof(double);
   a.lds_edges = bins <= (size_t)IPT_GRAPH_LDS_KB * 1024 ? 1 : 0;
   a.kd_tables = 0;  // the graph integrator never reads albedo
-  a.sample_major = IPT_GRAPH_SAMPLE_MAJOR;
+  a.sample_major = 1;
   return launch<MODE_GRAPH>(s, a, (a.lds_edges ? bins : 0) + table_bytes(a), nullptr, nullptr, nullptr, nullptr, target_dev, acc_dev,
                             (hipStream_t)stream);
 }
@@ -2287,11 +1982,20 @@ int gpu_selftest_math(uint64_t n, uint64_t seed, uint64_t *counts_host) {
 // megakernel's path cast (the culled one in small scenes); without targets
 // the brute-force loop returns the full closest hit.  Used by the exactness tests of the
 // BVH and of the shadow cull against the brute-force loop.
+// Potential-occluder mask of a shadow ray from a vertex on triangle `src`
+// towards emitter triangle `target` (all pairs when unknown: src < 0, or
+// target not an emitter -- the caller validates both).
+__device__ __forceinline__ uint32_t probe_allow(const uint32_t *masks, const int *emit_tri, int nE, int src,
+                                                int target) {
+  if (!masks || src < 0) return 0xffffffffu;
+  for (int e = 0; e < nE; ++e)
+    if (emit_tri[e] == target) return masks[src * nE + e];
+  return 0xffffffffu;
+}
+
 template <bool BVH>
 __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__restrict__ isect,
-                                                             const TriPair *__restrict__ pairs,
-                                                             const BvhNode *__restrict__ bnodes,
-                                                             const BvhPair *__restrict__ bpairs, const TraceArgs a,
+                                                             const TriPair *__restrict__ pairs, const TraceArgs a,
                                                              int small, int64_t n, const float *__restrict__ org,
                                                              const float *__restrict__ dir,
                                                              const int *__restrict__ targets,
@@ -2321,11 +2025,7 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
     }
   }
   BvhView bv;
-  bv.nodes = bnodes;
-  bv.pairs = bpairs;
   bv.isect = isect;
-  bv.lnodes = nullptr;
-  bv.stack = nullptr;
   bv.big = nullptr;
   bv.big_idx = nullptr;
   bv.big_e3 = nullptr;
@@ -2342,14 +2042,8 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
   for (int k = 0; k < 6; ++k) cv.root[k] = a.root_box[k];
   if (BVH) {
     char *base = reinterpret_cast<char *>(lds);
-    float4 *ln = reinterpret_cast<float4 *>(base + bvh_lds_offset((size_t)(small ? kE3Floats * nP : 0) * sizeof(float)));
-    if (a.bvh_lds_nodes > 0) {
-      const float4 *g = reinterpret_cast<const float4 *>(bnodes);
-      for (int i = tid; i < 4 * a.bvh_lds_nodes; i += kBlock) ln[i] = g[i];
-      bv.lnodes = ln;
-    }
-    float4 *lw = ln + 4 * a.bvh_lds_nodes;
-    if (kCoop && a.bvh_wide_lds > 0) {
+    float4 *lw = reinterpret_cast<float4 *>(base + bvh_lds_offset((size_t)(small ? kE3Floats * nP : 0) * sizeof(float)));
+    if (a.bvh_wide_lds > 0) {
       for (int i = tid; i < kWideF4 * a.bvh_wide_lds; i += kBlock) lw[i] = a.bvh_wide[i];
       cv.wn = lw;
       cv.wn_lds = true;
@@ -2366,31 +2060,26 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
     bv.nbig = a.bvh_nbig;
     uint32_t *after = reinterpret_cast<uint32_t *>(
         big_lds_copy(a, be3 + 6 * a.bvh_nbig, reinterpret_cast<float *>(lds), tid, kBlock, bv));
-    if (kCoop) cv.stk = after + (tid >> 6) * 8 * a.coop_stride;
-    else bv.stack = after + tid;
+    cv.stk = after + (tid >> 6) * 8 * a.coop_stride;
   }
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * kBlock + tid;
   const bool valid = i < n;  // no early return: the cooperative cast needs the whole wave
   V3 p = mk(0.f, 0.f, 0.f), d = mk(0.f, 0.f, 1.f);
-  int target = -1;
+  int target = -1, src = -1;
   if (valid) {
     p = mk(org[3 * i], org[3 * i + 1], org[3 * i + 2]);
     d = mk(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);
     target = targets ? targets[i] : -1;
+    src = sources ? sources[i] : -1;
   }
   float t = 0.f;
   int h = -1;
-  if (BVH && kCoop) {
+  if (BVH) {
     bool qn = false;
     if (valid) {
       if (target >= 0) {
-        uint32_t allow = 0xffffffffu;  // sources[i] >= 0: a vertex on that triangle (its occluder mask)
-        if (IPT_SHADOW_PO && sources && a.big_pomask && sources[i] >= 0) {
-          int e = 0;
-          while (e < a.nE - 1 && emit_tri[e] != target) ++e;
-          allow = a.big_pomask[sources[i] * a.nE + e];
-        }
+        const uint32_t allow = probe_allow(IPT_SHADOW_PO ? a.big_pomask : nullptr, emit_tri, a.nE, src, target);
         if (bvh_prepass<true>(bv, p, d, t, h, target, allow)) qn = coop_root_test(cv, p, d, t);
       } else {
         bvh_prepass<false>(bv, p, d, t, h, -1);
@@ -2400,20 +2089,14 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
     coop_cast<false>(cv, qn && target < 0, p, d, t, h);
     coop_cast<true>(cv, qn && target >= 0, p, d, t, h);
   } else if (valid) {
-    if (!BVH && IPT_SHADOW_CULL && small && target >= 0) {  // the megakernel's shadow cast of small scenes
-      uint32_t allow = 0xffffffffu;  // sources[i] >= 0: a vertex on that triangle (its occluder mask)
-      if (IPT_SHADOW_PO && sources && a.pomask && sources[i] >= 0) {
-        int e = 0;
-        while (e < a.nE - 1 && emit_tri[e] != target) ++e;
-        allow = a.pomask[sources[i] * a.nE + e];
-      }
-      h = shadow_hit_pairs_small((const lds_f32 *)lds_is, pairs, a.pboxes, e3, nT, p, d, target, t, allow,
-                                 IPT_PATH_CULL && IPT_SHADOW_TARGET_PAIR ? (const lds_f32 *)lds_pr : nullptr);
-    }
-    else if (!BVH && IPT_PATH_CULL && small && targets && target < 0)  // ... and its path cast
+    if (IPT_SHADOW_CULL && small && target >= 0) {  // the megakernel's shadow cast of small scenes
+      const uint32_t allow = probe_allow(IPT_SHADOW_PO ? a.pomask : nullptr, emit_tri, a.nE, src, target);
+      h = shadow_hit_pairs_small((const lds_f32 *)lds_is, pairs, a.pboxes, e3, nT, p, d, target, t, allow);
+    } else if (IPT_PATH_CULL && small && targets && target < 0) {  // ... and its path cast
       h = closest_hit_pairs_culled((const lds_f32 *)lds_pr, a.pboxes, nT, p, d, t);
-    else
-      h = cast<BVH>(isect, pairs, e3, nT, bv, p, d, t, target);
+    } else {  // the full closest hit (brute-force pair loop)
+      h = cast_bf(pairs, e3, nT, p, d, t);
+    }
   }
   if (valid) {
     t_out[i] = t;
@@ -2443,21 +2126,19 @@ int gpu_closest_hit(GpuScene *s, int64_t n, const float *org_dev, const float *d
   }
   if (n <= 0) return 0;
   TraceArgs a = make_args_scene(s);
-  const int small = (IPT_PAIRS && IPT_SMALL_UNROLL && s->host.nT <= 2 * kSmallPairs) ? 1 : 0;
+  const int small = s->host.nT <= 2 * kSmallPairs ? 1 : 0;
   const size_t base = small ? (size_t)kE3Floats * ((s->host.nT + 1) / 2) * sizeof(float) : 0;
   const int blocks = (int)((n + kBlock - 1) / kBlock);
   if (use_bvh(s)) {
-    const size_t lds = bvh_lds(s, a, base, false);
+    const size_t lds = bvh_lds(s, a, base);
     hipLaunchKernelGGL(closest_hit_kernel<true>, dim3(blocks), dim3(kBlock), lds, (hipStream_t)stream, s->isect,
-                       s->pairs, s->bnodes, s->bpairs, a, small, n, org_dev, dir_dev, targets_dev, sources_dev,
-                       s->emit_tri, t_dev, idx_dev);
+                       s->pairs, a, small, n, org_dev, dir_dev, targets_dev, sources_dev, s->emit_tri, t_dev, idx_dev);
   } else {
     const size_t lds = base + (small ? 12 + (size_t)s->host.nT * sizeof(TriIsect) +
                                            (IPT_PATH_CULL ? (size_t)((s->host.nT + 1) / 2) * sizeof(TriPair) : 0)
                                      : 0);
     hipLaunchKernelGGL(closest_hit_kernel<false>, dim3(blocks), dim3(kBlock), lds, (hipStream_t)stream, s->isect,
-                       s->pairs, s->bnodes, s->bpairs, a, small, n, org_dev, dir_dev, targets_dev, sources_dev,
-                       s->emit_tri, t_dev, idx_dev);
+                       s->pairs, a, small, n, org_dev, dir_dev, targets_dev, sources_dev, s->emit_tri, t_dev, idx_dev);
   }
   HIP_TRY(hipGetLastError());
   return 0;

@@ -39,7 +39,6 @@ struct HostScene {
   std::vector<PairBox2> bvh_big_boxes;  // their acceptance boxes (culled shadow pre-pass)
   // the same tree collapsed to 8-wide nodes for the cooperative traversal
   std::vector<WideNode> bvh_wide;   // breadth-first, root 0
-  std::vector<QWideNode> bvh_qwide; // the same nodes quantised (scene_layout.h)
   std::vector<TriIsect> bvh_wtris;  // leaf triangles (pad[0] = original index)
   int bvh_wdepth = 0;               // wide levels
   float bvh_root_box[6] = {0, 0, 0, 0, 0, 0};  // lo xyz, hi xyz of the whole tree

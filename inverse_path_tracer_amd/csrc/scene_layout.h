@@ -131,20 +131,6 @@ struct WideNode {
 };
 static_assert(sizeof(WideNode) == 256, "WideNode layout");
 constexpr int32_t kWideEmpty = (int32_t)0x80000000;
-// Quantised form of a WideNode (144 B instead of 256: the northstar scene's
-// 143-node tree fits the 32-KB LDS stage).  Per node a grid per axis, origin
-// o[a] and step 2^e[a] (biased exponent in byte a of `exps`); child k's box
-// is the grid box that CONTAINS its WideNode box (lo rounded down, hi up, 8
-// bits per bound), and o[a] + q * 2^e[a] is exact in fp32, so the decoded
-// boxes are supersets of the exact ones and the traversal still finds every
-// accepting triangle.  c[k] = {lo.x | lo.y << 8 | lo.z << 16 | hi.x << 24,
-// hi.y | hi.z << 8, ref, 0}.
-struct QWideNode {
-  float o[3];
-  uint32_t exps;
-  uint32_t c[8][4];
-};
-static_assert(sizeof(QWideNode) == 144, "QWideNode layout");
 
 // Acceptance boxes (bvh.cpp) of the brute-force loop's triangle pairs, two
 // pairs per record so one packed fma computes a slab parameter of both:

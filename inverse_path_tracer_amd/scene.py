@@ -186,14 +186,12 @@ class Scene:
         return nodes, pairs, big
 
     def export_wide(self):
-        """(wide[n,8,8] float32, qwide[n,36] uint32): the cooperative
-        traversal's 8-wide nodes and their quantised form (scene_layout.h)."""
+        """wide[n,8,8] float32: the cooperative traversal's 8-wide nodes
+        (WideNode, scene_layout.h; child refs are int32 bits)."""
         n = self.bvh_info()["wide_nodes"]
         wide = np.zeros((n, 8, 8), np.float32)
-        q = np.zeros((n, 36), np.uint32)
-        N.check(N.lib().ipt_scene_export_wide(self.handle, wide.ctypes.data_as(N.fp),
-                                              q.ctypes.data_as(C.POINTER(C.c_uint32))), "export_wide")
-        return wide, q
+        N.check(N.lib().ipt_scene_export_wide(self.handle, wide.ctypes.data_as(N.fp)), "export_wide")
+        return wide
 
     def closest_hit(self, origins, dirs, targets=None):
         """The kernels' cast on caller rays: (t float32[n], idx int32[n])."""

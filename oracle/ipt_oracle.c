@@ -1503,7 +1503,7 @@ static void edge_update(double *acc, int nT, int dst, int src, float w, const fl
   }
 }
 static void trace_graph(const oscene_t *sc, int W, int H, int spp, int max_bounces,
-                        uint64_t seed, int64_t gidx, const uint8_t *img, double *acc) {
+                        uint64_t seed, int64_t gidx, const uint8_t *img, double *acc, int64_t *casts) {
   xorwow_t st;
   xw_init(&st, seed + (uint64_t)gidx);
   int64_t pix = gidx / spp;
@@ -1517,6 +1517,7 @@ static void trace_graph(const oscene_t *sc, int W, int H, int spp, int max_bounc
   const double KW = ((1.0 / (double)INV_PI_F) / (double)P_RR) / (1.0 - 0.0);
   for (int k = 0;; k++) {
     hit_t h = intersect(sc, ray);
+    if (casts) (*casts)++;
     if (h.tri < 0) break;
     const otri_t *tri = &sc->tris[h.tri];
     (void)xw_uniform(&st); /* isSpecular = u < P_SPEC (= 0): always false */
@@ -1524,7 +1525,7 @@ static void trace_graph(const oscene_t *sc, int W, int H, int spp, int max_bounc
     edge_update(acc, sc->nT, dst, src, weight, pixel, zero, f0);
     v3 q = hit_point(ray, h.t);
     v3 nh = get_normal(tri, q);
-    nee_t ne = nee_geometry(sc, tri, q, nh, weight, &st, NULL);
+    nee_t ne = nee_geometry(sc, tri, q, nh, weight, &st, casts);
     if (ne.ok) {
       float w2 = (float)ne.g;
       edge_update(acc, sc->nT, src, ne.emitter, w2, pixel, sc->tris[ne.emitter].m.emission,
@@ -1568,6 +1569,40 @@ void oro_compress(int nT, const double *acc, float *data) {
   free(ws);
 }
 
+/* Casts (path + shadow) of createGraph's integrator over rows [row_begin,
+ * row_end): the C_bar of the graph roofline (bench.py).  The target image
+ * only weights the bins, never the paths, so none is needed. */
+int oro_graph_casts(void *p, int W, int H, int spp, int max_bounces, uint64_t seed, int row_begin, int row_end,
+                    int64_t *casts) {
+  oscene_t *sc = (oscene_t *)p;
+  if (!sc || !casts || row_begin < 0 || row_end > H || row_begin > row_end) {
+    set_err("bad graph arguments");
+    return -1;
+  }
+  size_t na = (size_t)(sc->nT + 1) * sc->nT * ACC_W;
+  int nth = nthreads();
+  double *accs = (double *)calloc(na * (size_t)nth, sizeof(double));
+  uint8_t *img = (uint8_t *)calloc((size_t)W * H * 3, 1);
+  int64_t b = (int64_t)row_begin * W * spp, e = (int64_t)row_end * W * spp, total = 0;
+#pragma omp parallel num_threads(nth) reduction(+ : total)
+  {
+#ifdef _OPENMP
+    int tid = omp_get_thread_num();
+    int nt = omp_get_num_threads();
+#else
+    int tid = 0, nt = 1;
+#endif
+    int64_t chunk = (e - b + nt - 1) / nt;
+    int64_t lo = b + chunk * tid, hi = lo + chunk < e ? lo + chunk : e;
+    for (int64_t g = lo; g < hi; g++)
+      trace_graph(sc, W, H, spp, max_bounces, seed, g, img, accs + na * (size_t)tid, &total);
+  }
+  *casts = total;
+  free(img);
+  free(accs);
+  return 0;
+}
+
 int oro_graph(void *p, int W, int H, int spp, int max_bounces, uint64_t seed, int row_begin,
               int row_end, const uint8_t *target, double *acc_out, float *data) {
   oscene_t *sc = (oscene_t *)p;
@@ -1591,7 +1626,7 @@ int oro_graph(void *p, int W, int H, int spp, int max_bounces, uint64_t seed, in
     int64_t chunk = (n + nt - 1) / nt;
     int64_t lo = b + chunk * tid, hi = lo + chunk < e ? lo + chunk : e;
     for (int64_t g = lo; g < hi; g++)
-      trace_graph(sc, W, H, spp, max_bounces, seed, g, target, accs + na * (size_t)tid);
+      trace_graph(sc, W, H, spp, max_bounces, seed, g, target, accs + na * (size_t)tid, NULL);
   }
   double *acc = acc_out ? acc_out : (double *)malloc(na * sizeof(double));
   for (size_t i = 0; i < na; i++) {

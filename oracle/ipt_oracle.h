@@ -70,6 +70,8 @@ void oro_pixel_mean(const float *samples, int64_t npix, int spp, float *hdr,
  * target: H*W*3 RGB8.  acc (nullable): (nT+1)*nT*8 doubles
  * [w, f0, pix0 rgb, light0 rgb] per (dst,src).  data: (nT+1)*nT*7 floats in
  * the createGraph layout (ipt_cuda.py:145-163). */
+int oro_graph_casts(void *scene, int W, int H, int spp, int max_bounces, uint64_t seed, int row_begin,
+                    int row_end, int64_t *casts);
 int oro_graph(void *scene, int W, int H, int spp, int max_bounces,
               uint64_t seed, int row_begin, int row_end,
               const uint8_t *target, double *acc, float *data);

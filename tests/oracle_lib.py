@@ -55,6 +55,8 @@ def _bind(L):
     L.oro_render_samples.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, i64, i64, fp, C.POINTER(i64)]
     L.oro_pixel_mean.argtypes = [fp, i64, C.c_int, fp, C.POINTER(C.c_uint8)]
     L.oro_graph.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int, C.c_int, C.POINTER(C.c_uint8), dp, fp]
+    L.oro_graph_casts.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int, C.c_int,
+                                  C.POINTER(C.c_int64)]
     L.oro_compress.argtypes = [C.c_int, dp, fp]
     L.oro_adjoint.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int, C.c_int, fp, dp]
     L.oro_uniform_at.restype = C.c_float
@@ -151,6 +153,16 @@ class OracleScene:
         if rc:
             raise RuntimeError(self.L.oro_last_error().decode())
         return acc, data
+
+    def graph_casts(self, W, H, spp, max_bounces, seed, row_begin=0, row_end=None):
+        """Path + shadow casts of createGraph's integrator over rows [row_begin, row_end)."""
+        row_end = H if row_end is None else row_end
+        n = C.c_int64(0)
+        rc = self.L.oro_graph_casts(self.ptr, W, H, spp, -1 if max_bounces is None else max_bounces, seed,
+                                    row_begin, row_end, C.byref(n))
+        if rc:
+            raise RuntimeError(self.L.oro_last_error().decode())
+        return n.value
 
     def adjoint(self, W, H, spp, max_bounces, seed, adj, row_begin=0, row_end=None):
         row_end = H if row_end is None else row_end

@@ -270,38 +270,29 @@ def test_never_hit_triangle_left_out(tmp_path):
 
 
 @pytest.mark.parametrize("name", ["sphere", "clutter", "northstar"])
-def test_quantised_wide_nodes_contain_exact_boxes(name):
-    """QWideNode (scene_layout.h): every decoded child box o + q * 2^e is an
-    exactly representable float box that contains the WideNode child box,
-    with the same child reference; empty slots stay empty (lo > hi)."""
+def test_wide_nodes_nest_and_order_children(name):
+    """WideNode (scene_layout.h, bvh.cpp build_wide): every inner child's own
+    children lie inside the box its parent slot stores, and each slot's pad
+    word is a permutation of the 8 children (the octant front-to-back order
+    the cooperative traversal's lane j reads)."""
     from conftest import NORTHSTAR
 
     recs = {"sphere": SPHERE_SCENE, "clutter": CLUTTER_SCENE, "northstar": NORTHSTAR}[name]
     P = product_scene(recs, device=False)
-    wide, q = P.export_wide()
+    wide = P.export_wide()
     assert len(wide) == P.bvh_info()["wide_nodes"] > 0
     if name == "northstar":
-        assert len(q) * 256 <= 32 * 1024  # the sphere-only tree (cube in the pre-pass) fits the LDS stage
-    o = q[:, :3].copy().view(np.float32).astype(np.float64)
-    e = np.stack([(q[:, 3] >> (8 * a)) & 0xFF for a in range(3)], 1).astype(np.int64) - 127
-    step = np.ldexp(1.0, e)
+        assert len(wide) * 256 <= 32 * 1024  # the sphere-only tree (cube in the pre-pass) fits the LDS stage
     refs = wide[:, :, 6].copy().view(np.int32)
-    c = q[:, 4:].reshape(-1, 8, 4)
-    assert np.array_equal(c[:, :, 2].view(np.int32), refs)
     used = refs != np.int32(-2 ** 31)
-    w0, w1 = c[:, :, 0].astype(np.int64), c[:, :, 1].astype(np.int64)
-    ql = np.stack([w0 & 255, (w0 >> 8) & 255, (w0 >> 16) & 255], -1)
-    qh = np.stack([w0 >> 24, w1 & 255, (w1 >> 8) & 255], -1)
-    lo = o[:, None, :] + ql * step[:, None, :]
-    hi = o[:, None, :] + qh * step[:, None, :]
-    # exact in float32 (the device's fmaf decode rounds nothing)
-    assert np.array_equal(lo.astype(np.float32).astype(np.float64), lo)
-    assert np.array_equal(hi.astype(np.float32).astype(np.float64), hi)
-    exact_lo, exact_hi = wide[:, :, 0:3].astype(np.float64), wide[:, :, 3:6].astype(np.float64)
-    assert np.all(lo[used] <= exact_lo[used]) and np.all(hi[used] >= exact_hi[used])
-    assert np.all(ql[~used][:, 0] > qh[~used][:, 0])
-    # tight: each bound within one grid step of the exact one
-    assert np.all(exact_lo[used] - lo[used] < np.broadcast_to(step[:, None, :], lo.shape)[used])
+    for n in range(len(wide)):
+        for k in np.nonzero(used[n] & (refs[n] >= 0))[0]:
+            c = refs[n, k]
+            cu = used[c]
+            assert np.all(wide[c, cu, 0:3] >= wide[n, k, 0:3]) and np.all(wide[c, cu, 3:6] <= wide[n, k, 3:6])
+        for o in range(8):
+            perm = int(wide[n, o, 7:8].copy().view(np.uint32)[0])
+            assert sorted((perm >> (3 * r)) & 7 for r in range(8)) == list(range(8))
 
 
 def _shadow_rays(tris, n, rng, edge_frac=0.3):

@@ -26,5 +26,14 @@ for name, (recs, W, H, spp, mb, seed) in CONFIGS.items():
         n += len(s)
     out[name] = {"casts_per_sample": total / n, "samples": n, "nT": sc.nT, "seconds": round(time.time() - t0, 1)}
     print(name, out[name], flush=True)
+# createGraph at the reference's own configuration (scene.h:8-11: 500x500,
+# 100 spp, no bounce cap; scenes/0.txt): its integrator draws isSpecular at
+# every vertex, so its paths differ from the forward's -- counted separately
+sc = O.OracleScene(SCENE0)
+t0 = time.time()
+c = sc.graph_casts(500, 500, 100, None, 0)
+out["graph_scene0_500x500x100_unbounded"] = {"casts_per_sample": c / (500 * 500 * 100), "samples": 500 * 500 * 100,
+                                             "nT": sc.nT, "seconds": round(time.time() - t0, 1)}
+print("graph", out["graph_scene0_500x500x100_unbounded"], flush=True)
 with open(os.path.join(ROOT, "profiles", "casts_per_sample.json"), "w") as f:
     json.dump(out, f, indent=1)

@@ -17,7 +17,12 @@ NAMES = ["refill", "path_cast", "shade", "shadow_cast", "emitter_eval", "finalis
 
 
 def main():
-    L = VB.load(os.path.join(VB.ROOT, "inverse_path_tracer_amd/lib/variants/libipt_phase.so"))
+    for lib in os.environ.get("IPT_PHASE_LIBS", "phase").split(","):
+        run(lib)
+
+
+def run(lib):
+    L = VB.load(os.path.join(VB.ROOT, "inverse_path_tracer_amd/lib/variants/libipt_%s.so" % lib))
     L.ipt_debug_phase_cycles.argtypes = [C.POINTER(C.c_ulonglong)]
     torch.cuda.set_device(0)
     dev = torch.device("cuda:0")
@@ -45,8 +50,8 @@ def main():
             res["iterations_per_wave_total"] = v[6]
             res["mean_active_lanes"] = round(v[7] / max(1, v[6]), 2)
             res["cycles_total"] = tot
-            out["%s:%s" % (sname, kind)] = res
-            print(sname, kind, json.dumps(res), flush=True)
+            out["%s:%s:%s" % (lib, sname, kind)] = res
+            print(lib, sname, kind, json.dumps(res), flush=True)
     print(json.dumps(out))
 
 

@@ -64,13 +64,14 @@ def main():
     names = sys.argv[1:] or sorted(os.path.basename(p)[7:-3] for p in glob.glob(os.path.join(ROOT, "inverse_path_tracer_amd/lib/variants/libipt_*.so")))
     libs = {n: load(os.path.join(ROOT, "inverse_path_tracer_amd/lib/variants/libipt_%s.so" % n)) for n in names}
     ref = load(N.LIB_PATH)
+    libs["cur"] = ref  # the default build is timed next to the variants
     torch.cuda.set_device(0)
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream().cuda_stream
     out = {}
     for sname, recs in SCENES.items():
         hs = {n: scene(L, recs) for n, L in libs.items()}
-        href = scene(ref, recs)
+        href = hs["cur"]
         # correctness: small frame bit-exact vs default library
         p = N.make_params(64, 64, 8, 4, 123)
         want = np.zeros((64 * 64 * 8, 3), np.float32)
@@ -79,6 +80,16 @@ def main():
             got = np.zeros_like(want)
             assert L.ipt_render_samples_host(hs[n], C.byref(p), got.ctypes.data_as(N.fp)) == 0
             print(sname, n, "bit-exact" if np.array_equal(got.view(np.uint32), want.view(np.uint32)) else "MISMATCH", flush=True)
+        # adjoint: fp64 sums, equal to the default library's up to summation order
+        adj_s = np.random.RandomState(5).uniform(-1, 1, (64, 64, 3)).astype(np.float32)
+        nt = ref.ipt_scene_num_triangles(href)
+        gw = np.zeros((nt, 3), np.float64)
+        assert ref.ipt_adjoint_host(href, C.byref(p), adj_s.ctypes.data_as(N.fp), gw.ctypes.data_as(N.dp)) == 0
+        for n, L in libs.items():
+            gg = np.zeros_like(gw)
+            assert L.ipt_adjoint_host(hs[n], C.byref(p), adj_s.ctypes.data_as(N.fp), gg.ctypes.data_as(N.dp)) == 0
+            err = float(np.max(np.abs(gg - gw)) / max(np.max(np.abs(gw)), 1e-300))
+            print(sname, n, "adjoint max rel diff %.2e" % err, "OK" if err < 1e-9 else "MISMATCH", flush=True)
         p = N.make_params(512, 512, 64, 4, 0)
         buf = torch.empty((512 * 512 * 64, 3), device=dev)
         adj = torch.ones((512, 512, 3), device=dev)
