@@ -923,19 +923,23 @@ __device__ __forceinline__ float wave_shl1(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
 }
 
+// Minimum of a 32-bit int over the 8 lanes of each group: three DPP stages
+// (quad_perm [1,0,3,2]: lane ^ 1, [2,3,0,1]: lane ^ 2, row_half_mirror: the
+// other quad), each fused by the compiler into one v_min_i32_dpp.
 template <int CTRL>
-__device__ __forceinline__ void lexmin_dpp(float &t, int &i) {
-  const float t2 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(t), CTRL, 0xf, 0xf, false));
-  const int i2 = __builtin_amdgcn_update_dpp(0, i, CTRL, 0xf, 0xf, false);
-  const bool take = (t2 < t) | ((t2 == t) & (i2 < i));
-  t = take ? t2 : t;
-  i = take ? i2 : i;
+__device__ __forceinline__ int min_dpp(int v) {
+  return min(v, __builtin_amdgcn_update_dpp(0x7fffffff, v, CTRL, 0xf, 0xf, false));
 }
-// Lexicographic minimum of (t, i) over the 8 lanes of each group.
+__device__ __forceinline__ int group_min_i32(int v) { return min_dpp<0x141>(min_dpp<0x4E>(min_dpp<0xB1>(v))); }
+// Lexicographic minimum of (t, i) over the 8 lanes of each group.  Every t
+// here is an accepted hit parameter (>= kEpsUp) or +inf, never NaN or
+// negative, so its bit pattern orders like its value: the minimum t is an
+// integer minimum of the bits, then the minimum index among the lanes that
+// hold it (7 VALU instead of ~21 for a (t, i) compare-select per stage).
 __device__ __forceinline__ void group_lexmin(float &t, int &i) {
-  lexmin_dpp<0xB1>(t, i);   // quad_perm [1,0,3,2]: partner lane ^ 1
-  lexmin_dpp<0x4E>(t, i);   // quad_perm [2,3,0,1]: partner lane ^ 2
-  lexmin_dpp<0x141>(t, i);  // row_half_mirror: lane 7 - i, the other quad of the group
+  const int tb = group_min_i32(__float_as_int(t));
+  i = group_min_i32(__float_as_int(t) == tb ? i : 0x7fffffff);
+  t = __int_as_float(tb);
 }
 __device__ __forceinline__ float bperm_f(int addr, float v) {
   return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v)));
@@ -969,8 +973,8 @@ __device__ __forceinline__ float tri_accept_t(const TriIsect &T, V3 p, V3 d) {
 
 // Cooperative closest hit.  Called by ALL 64 lanes of the wave (convergent);
 // lanes with `need` have their (bt, bi) continued through the tree
-// lexicographically.  SHADOW: the entry bi is the target emitter; a group
-// stops as soon as its bi is no longer the target (occluded).
+// lexicographically.  SHADOW: the lanes' entry bi is the target emitter; a
+// group stops as soon as its bi is no longer the target (occluded).
 template <bool SHADOW>
 __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3 d, float &bt, int &bi) {
 #ifdef IPT_ABL_NOTRAV  // timing-only ablation build: pre-pass only, no traversal

@@ -196,6 +196,11 @@ struct TraceArgs {
   // until the launch's items are used up; chunk 0 = static per-wave ranges
   uint32_t chunk;
   uint32_t *chunk_ctr;
+  // value of every set's counter when this launch starts: the counters are
+  // never reset (no memset launch per launch) -- a launch grabs exactly
+  // max(chunks - waves, 0) + waves times per set (each wave grabs until one
+  // grab fails), so the host knows the next launch's base (stream_counters)
+  uint32_t chunk_base;
   // small scenes: acceptance boxes of the pairs (culled shadow casts)
   const PairBox2 *pboxes;
   // small scenes: potential occluders per (source triangle, emitter), nT*nE
@@ -328,8 +333,13 @@ constexpr int min_blocks() {
 // (r02_variants_adj_sweep.log), quantised wide nodes (r02_variants_qnodes.log),
 // the forward's camera-ray ring (r02_variants_occupancy_after_cull.log), the
 // shadow target tested with its pair partner (r02_variants_shadow_target_pair.log)
-// and the tolerance-mode fast cast (r02_variants_fastcast.log: fails the
-// 1e-3 gradient bar).
+// the tolerance-mode fast cast (r02_variants_fastcast.log: fails the
+// 1e-3 gradient bar), a per-wave LDS queue that parked the forward's path
+// rays with their path state until a full cooperative round of 8 was waiting
+// (r03/variants_queue_chsweep_r03f.log: north-star forward 4.70 vs 3.75 ms;
+// r03/variants_r03e.log for the first form, 4.30 ms) and a channel-split
+// adjoint sweep, lane 3i + c walking path i in channel c (same log: C2
+// adjoint 2.33 vs 2.16 ms, north-star 6.57 vs 5.02 ms at one wave less).
 // Graph bins stay in LDS up to this size (KB), else global fp64 atomics.
 #ifndef IPT_GRAPH_LDS_KB
 #define IPT_GRAPH_LDS_KB 64
@@ -607,7 +617,6 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   V3 pix = p;          // GRAPH target pixel
   int k = 0, dst = 0;
   uint64_t witem = 0;  // this lane's work item (output slot / pixel source)
-
   // One iteration = one path vertex for the whole wave, in two
   // wave-synchronous phases: (1) every active lane casts its path ray and,
   // on a hit, shades the vertex and draws ALL of the vertex's random numbers
@@ -646,7 +655,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       // (profiles/r02_variants_chunk_*.log): 8 counters on separate lines
       // with stealing and a grab prefetched one chunk ahead were both slower.
       uint32_t c = 0;
-      if (lane == 0) c = atomicAdd(a.chunk_ctr + set, 1u);
+      if (lane == 0) c = atomicAdd(a.chunk_ctr + set, 1u) - a.chunk_base;
       c = (uint32_t)__shfl((int)c, 0);
       const uint64_t start = (uint64_t)(nwaves + c) * a.chunk;
       if (start < a.n_samples) {
@@ -756,7 +765,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         bvh_prepass<false>(bv, p, d, t, hit, -1);
         qn = coop_root_test(cv, p, d, t);
       }
+#ifndef IPT_ABL_NOTRAV_PATH  // timing-only ablation: path rays skip the tree
       coop_cast<false>(cv, qn, p, d, t, hit);
+#endif
     } else if (active) {
       if (IPT_PATH_CULL && e3)
         hit = closest_hit_pairs_culled((const lds_f32 *)lds_pr, a.pboxes, nT, p, d, t);
@@ -871,7 +882,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         if (shadow && bvh_prepass<true>(bv, p, sd, ts, hs, et,
                                         a.big_pomask ? a.big_pomask[tri * nE + emitter] : 0xffffffffu, emitter))
           qn = coop_root_test(cv, p, sd, ts);
+#ifndef IPT_ABL_NOTRAV_SHADOW  // timing-only ablation: shadow rays skip the tree
         coop_cast<true>(cv, qn, p, sd, ts, hs);
+#endif
       } else if (shadow) {
         if (IPT_SHADOW_CULL && e3)
           hs = shadow_hit_pairs_small((const lds_f32 *)lds_is, pairs, a.pboxes, e3, nT, p, sd, et, ts,
@@ -1218,7 +1231,6 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   if ((tid & 63) == 0)
     for (int i = 0; i < 8; ++i) atomicAdd(&g_phase_cycles[i], (unsigned long long)tacc[i]);
 #endif
-
   }
 
   if (MODE != MODE_FWD) {
@@ -1336,6 +1348,16 @@ struct GpuScene {
   size_t grid_lds[16] = {0};
   size_t pick_base[16] = {0};  // launch_bvh's LDS choice per (mode, spec): base bytes it was made for
   int pick_opt[16] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+  // dynamic-chunk counters per (stream, number of sets): zeroed once, then
+  // advanced by every launch by a known amount (TraceArgs::chunk_base)
+  struct Counters {
+    hipStream_t stream;
+    int sets;
+    uint32_t *dev;
+    uint32_t base;
+  };
+  std::vector<Counters> counters;
+  std::mutex counters_mu;
 };
 
 #ifdef IPT_PHASE_TIMING
@@ -1462,6 +1484,7 @@ void gpu_free(GpuScene *s) {
   (void)hipFree(s->big_pomask);
   (void)hipFree(s->grad_map);
   (void)hipFree(s->slot_tri);
+  for (auto &c : s->counters) (void)hipFree(c.dev);
   delete s;
 }
 
@@ -1582,6 +1605,7 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.rec_cap = p.max_bounces >= 0 ? p.max_bounces + 1 : 0;
   a.chunk = 0;
   a.chunk_ctr = nullptr;
+  a.chunk_base = 0;
   a.pboxes = s->pboxes;
   a.pomask = s->host.nE > 0 ? s->pomask : nullptr;
   a.big_pomask = nullptr;  // set with the other BVH fields (bvh_lds)
@@ -1652,6 +1676,43 @@ struct StreamScratch {
   }
 };
 
+// The chunk counters of a launch with `sets` material sets on stream `st`:
+// allocated and zeroed once per (stream, sets) and never reset -- each launch
+// adds exactly grabs_per_set to every set's counter (TraceArgs::chunk_base),
+// so the host returns the base this launch starts from and advances it.
+// Launches on one stream run in order; other streams get their own counters.
+// *lk holds the scene's counter lock until the caller has enqueued the launch,
+// so host threads sharing a stream enqueue in the order of their bases.
+// A launch captured into a graph (replayed without this host step) gets
+// fresh zeroed counters of its own instead (*scratch, freed behind it).
+static int stream_counters(GpuScene *s, hipStream_t st, int sets, uint32_t grabs_per_set, uint32_t **out,
+                           uint32_t *base, void **scratch, std::unique_lock<std::mutex> *lk) {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  HIP_TRY(hipStreamIsCapturing(st, &cap));
+  if (cap != hipStreamCaptureStatusNone) {
+    HIP_TRY(hipMallocAsync(scratch, (size_t)sets * sizeof(uint32_t), st));
+    HIP_TRY(hipMemsetAsync(*scratch, 0, (size_t)sets * sizeof(uint32_t), st));
+    *out = (uint32_t *)*scratch;
+    *base = 0;
+    return 0;
+  }
+  *lk = std::unique_lock<std::mutex>(s->counters_mu);
+  GpuScene::Counters *c = nullptr;
+  for (auto &e : s->counters)
+    if (e.stream == st && e.sets == sets) c = &e;
+  if (!c) {
+    uint32_t *dev = nullptr;
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&dev), (size_t)sets * sizeof(uint32_t)));
+    HIP_TRY(hipMemset(dev, 0, (size_t)sets * sizeof(uint32_t)));
+    s->counters.push_back({st, sets, dev, 0u});
+    c = &s->counters.back();
+  }
+  *out = c->dev;
+  *base = c->base;
+  c->base += grabs_per_set;  // (mod 2^32: the kernel subtracts in uint32)
+  return 0;
+}
+
 template <int MODE, bool SPEC, bool BVH>
 static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float *kd_dev, float *out, const float *adj,
                        double *grad, const uint8_t *target, double *edges, hipStream_t st) {
@@ -1667,19 +1728,22 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
     b.bps = std::max(1, grid / a.nscenes);
     grid = b.bps * a.nscenes;
   }
-  StreamScratch ctr;
   b.chunk = 0;
   b.chunk_ctr = nullptr;
+  b.chunk_base = 0;
+  StreamScratch cap_ctr;  // only for a launch captured into a graph
+  std::unique_lock<std::mutex> ctr_lock;  // released after the launch is enqueued
   if (IPT_DYN_CHUNKS) {
     // ~IPT_DYN_CHUNKS_PER_WAVE chunks per wave, a multiple of 64 items, 64..4096
     const uint64_t waves = (uint64_t)(a.nscenes > 1 ? b.bps : grid) * (kBlock / 64);
     uint64_t c = (a.n_samples / (waves * IPT_DYN_CHUNKS_PER_WAVE) + 63) / 64 * 64;
     c = std::min<uint64_t>(std::max<uint64_t>(c, IPT_DYN_MIN_CHUNK), 4096);
     b.chunk = (uint32_t)c;
-    const size_t bytes = (size_t)a.nscenes * sizeof(uint32_t);
-    if (ctr.alloc(bytes, st)) return -1;
-    HIP_TRY(hipMemsetAsync(ctr.p, 0, bytes, st));
-    b.chunk_ctr = (uint32_t *)ctr.p;
+    const uint64_t chunks = (a.n_samples + c - 1) / c;
+    const uint64_t grabs = (chunks > waves ? chunks - waves : 0) + waves;  // per set, see TraceArgs::chunk_base
+    cap_ctr.st = st;
+    if (stream_counters(s, st, a.nscenes, (uint32_t)grabs, &b.chunk_ctr, &b.chunk_base, &cap_ctr.p, &ctr_lock))
+      return -1;
   }
   hipLaunchKernelGGL((trace_kernel<MODE, SPEC, BVH>), dim3(grid), dim3(kBlock), lds, st, b, s->isect, s->pairs, s->geom,
                      s->mat, kd_dev ? kd_dev : s->kd, s->emit_tri, s->emit_cdf, s->emit_pmf, out, adj, grad, target,

@@ -22,6 +22,7 @@
 #   phase        tools/phase_timing.py
 #   stats        tools/bvh_stats.py with the IPT_BVH_STATS variant library ($SCENES)
 #   multirank    2-rank gloo rehearsal of bench.py on the one GPU
+#   scaling      tools/launch_scaling.py (fixed cost per launch: C2 shares 1/1 .. 1/64)
 #   workflow     tools/workflow_at_size.py (pipeline all --n 100 + optimize --n 100)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -75,6 +76,7 @@ run() {
     multirank) IPT_BENCH_DEVICE=0 IPT_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 \
                    --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 40 \
                    --warmup 4 > "$OUT/bench_2rank_$T.json" 2> "$OUT/bench_2rank_$T.err" ;;
+    scaling) timeout -k 10 300 python tools/launch_scaling.py > "$OUT/scaling_$T.jsonl" 2> "$OUT/scaling_$T.err" ;;
     workflow) timeout -k 10 1000 python -u tools/workflow_at_size.py --out "$OUT/workflow_$T.json" > "$OUT/workflow_$T.log" 2>&1 ;;
     *) echo "unknown stage $1" >&2; return 2 ;;
   esac
