@@ -62,10 +62,15 @@ const char *gpu_last_error() { return g_gpu_err.c_str(); }
 // is swept in chunks from its end, each earlier chunk re-recorded by
 // replaying the path from its camera ray (same seed, same draws, so the same
 // floats) -- see trace_kernel.
-enum { MODE_FWD = 0, MODE_ADJ = 1, MODE_GRAPH = 2, MODE_ADJU = 3 };
+// MODE_FWDM: MODE_FWD with the pixel mean fused in (gpu_render, TraceArgs::fused).
+enum { MODE_FWD = 0, MODE_ADJ = 1, MODE_GRAPH = 2, MODE_ADJU = 3, MODE_FWDM = 4 };
 template <int MODE>
 constexpr bool is_adj() {
   return MODE == MODE_ADJ || MODE == MODE_ADJU;
+}
+template <int MODE>
+constexpr bool is_fwd() {
+  return MODE == MODE_FWD || MODE == MODE_FWDM;
 }
 constexpr int kBlock = 256;
 // Adjoint vertex record (per lane, in LDS): tri | et << 16, the emitter factor
@@ -208,6 +213,15 @@ struct TraceArgs {
   const uint32_t *pomask;
   // BVH scenes: the same masks over the large-triangle pairs (nullptr = none)
   const uint32_t *big_pomask;
+  // FWD with the pixel mean fused in (gpu_render, IPT_FUSED_MEAN): work comes
+  // in chunks of fused_p (= 2^fused_shift) launch-local pixels x spp samples;
+  // a finished sample goes to its chunk's slot in the wave's LDS (two slots
+  // per wave, mean_slot floats each, at byte mean_off of the dynamic LDS),
+  // and when the last sample of a chunk is in, the wave sums each pixel's
+  // samples in sample order (toneMap) into out_samples (HDR, npix x 3) and ldr
+  int fused, fused_p, fused_shift;
+  uint32_t mean_off, mean_slot;
+  uint8_t *ldr;
 };
 static_assert(alignof(TraceArgs) == 8, "TraceArgs sits right after the ten 8-B scene pointers in the kernarg segment");
 
@@ -267,10 +281,8 @@ using namespace dev;
 // Work item w of a launch -> global sample g, pixel (r, c), XORWOW state
 // after the two camera draws and the camera ray (path_trace.cu:150-165); the
 // enumeration is described in trace_kernel.
-__device__ __forceinline__ void item_ray(const TraceArgs &a, uint64_t seed, uint64_t w, Rng &st, V3 &p, V3 &d, int &r,
-                                         int &c) {
-  uint64_t lp, sj;
-  item_split(a, w, lp, sj);
+__device__ __forceinline__ void item_ray_ls(const TraceArgs &a, uint64_t seed, uint64_t lp, uint64_t sj, Rng &st, V3 &p,
+                                            V3 &d, int &r, int &c) {
   local_rc(a, lp, r, c);
   uint64_t g;  // global sample index
   if (a.idx32) {  // every index of the frame fits 32 bits: one 32x32->64 multiply-add
@@ -281,6 +293,12 @@ __device__ __forceinline__ void item_ray(const TraceArgs &a, uint64_t seed, uint
   }
   rng_init(st, seed + g);
   camera_ray(a.cam, a.cam_org, st, r, c, a.W, a.H, a.rc_W, a.rc_H, p, d);
+}
+__device__ __forceinline__ void item_ray(const TraceArgs &a, uint64_t seed, uint64_t w, Rng &st, V3 &p, V3 &d, int &r,
+                                         int &c) {
+  uint64_t lp, sj;
+  item_split(a, w, lp, sj);
+  item_ray_ls(a, seed, lp, sj, st, p, d, r, c);
 }
 
 // ---------------------------------------------------------------------------
@@ -322,8 +340,8 @@ __device__ __forceinline__ void item_ray(const TraceArgs &a, uint64_t seed, uint
 #endif
 template <int MODE, bool BVH>
 constexpr int min_blocks() {
-  return BVH ? (is_adj<MODE>() ? IPT_MIN_BLOCKS_BVH_ADJ : (MODE == 0 ? IPT_MIN_BLOCKS_BVH_FWD : IPT_MIN_BLOCKS_BVH))
-             : (MODE == 0 ? IPT_MIN_BLOCKS_FWD : (is_adj<MODE>() ? IPT_MIN_BLOCKS_ADJ : IPT_MIN_BLOCKS_GRAPH));
+  return BVH ? (is_adj<MODE>() ? IPT_MIN_BLOCKS_BVH_ADJ : (is_fwd<MODE>() ? IPT_MIN_BLOCKS_BVH_FWD : IPT_MIN_BLOCKS_BVH))
+             : (is_fwd<MODE>() ? IPT_MIN_BLOCKS_FWD : (is_adj<MODE>() ? IPT_MIN_BLOCKS_ADJ : IPT_MIN_BLOCKS_GRAPH));
 }
 // Rejected and removed (round 3; the A/B logs under profiles/ keep the
 // evidence): a traversal-server wave per workgroup fed through an LDS ray
@@ -437,7 +455,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   const uint64_t seed = a.seed + (uint64_t)set * a.seed_stride;
   if (a.nscenes > 1) {
     kd += (size_t)set * 3 * a.nT;
-    if (MODE == MODE_FWD) out_samples += (size_t)set * a.out_stride;
+    if (is_fwd<MODE>()) out_samples += (size_t)set * a.out_stride;
     if (is_adj<MODE>()) {
       adj += (size_t)set * a.adj_stride;
       grad += (size_t)set * 3 * a.nT;
@@ -604,6 +622,14 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     end = (a.n_samples * (wave + 1)) / nwaves;
   }
   bool exhausted = !dyn;
+  // fused pixel mean (MODE_FWDM): the two LDS slots' launch-local first pixel
+  // and items not yet finished; fst bit 0 = the slot being issued, bit 1 =
+  // the wave has taken its first chunk; fj = items of that slot issued so
+  // far (item j = sample j / np of pixel first + j % np, np = the chunk's
+  // pixels: sample-major inside the chunk).  Few registers: the pixel count
+  // is recomputed from the first pixel (only a launch's last chunk is short).
+  uint32_t f0lp = 0, f1lp = 0, fj = 0;
+  int fl0 = 0, fl1 = 0, fst = 1;
 
   bool active = false;
   Rng st;
@@ -650,7 +676,44 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     asm volatile("" : "+s"(apc));
     const TraceArgs a = *apc;
 #endif
-    if (next >= end && !exhausted) {  // wave-uniform: the next chunk (full exec here)
+    if (MODE == MODE_FWDM) {
+      // the current chunk is fully issued and the other slot is free: the
+      // next chunk goes there (first the wave's own, then from the counter)
+      const uint32_t clp = (fst & 1) ? f1lp : f0lp;
+      const uint64_t cleft = a.npix - clp;
+      const uint32_t cn = (uint32_t)(cleft < (uint64_t)a.fused_p ? cleft : (uint64_t)a.fused_p) * (uint32_t)a.spp;
+      if ((!(fst & 2) || fj >= cn) && !exhausted && ((fst & 1) ? fl0 : fl1) == 0) {
+        // (a wave whose own chunk is past the end grabs once, as in the
+        // unfused protocol: every wave's last grab fails, TraceArgs::chunk_base)
+        uint32_t blk = wave;
+        bool own = false;
+        if (!(fst & 2)) {
+          fst |= 2;
+          own = ((uint64_t)blk << a.fused_shift) < a.npix;
+        }
+        if (!own) {
+          uint32_t c = 0;
+          if (lane == 0) c = atomicAdd(a.chunk_ctr + set, 1u) - a.chunk_base;
+          blk = nwaves + (uint32_t)__builtin_amdgcn_readfirstlane((int)c);  // lane 0 (full exec here)
+        }
+        const uint64_t lp0 = (uint64_t)blk << a.fused_shift;
+        if (lp0 < a.npix) {
+          const uint64_t left = a.npix - lp0;
+          const int n = (left < (uint64_t)a.fused_p ? (int)left : a.fused_p) * a.spp;
+          fst ^= 1;
+          if (fst & 1) {
+            f1lp = (uint32_t)lp0;
+            fl1 = n;
+          } else {
+            f0lp = (uint32_t)lp0;
+            fl0 = n;
+          }
+          fj = 0;
+        } else {
+          exhausted = true;
+        }
+      }
+    } else if (next >= end && !exhausted) {  // wave-uniform: the next chunk (full exec here)
       // One counter, grabbed when needed.  Measured against alternatives
       // (profiles/r02_variants_chunk_*.log): 8 counters on separate lines
       // with stealing and a grab prefetched one chunk ahead were both slower.
@@ -719,7 +782,33 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     }
     // ---- refill finished lanes from the wave's range (ballot + mbcnt)
     const uint64_t need = RING ? 0ull : __ballot(!active);
-    if (need) {
+    if (MODE == MODE_FWDM) {
+      const uint32_t clp = (fst & 1) ? f1lp : f0lp;
+      const uint64_t cleft = a.npix - clp;
+      const uint32_t np = (uint32_t)(cleft < (uint64_t)a.fused_p ? cleft : (uint64_t)a.fused_p);
+      const uint32_t fn = np * (uint32_t)a.spp;
+      if (need && (fst & 2) && fj < fn) {
+        const uint32_t rank =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+        if (!active && fj + rank < fn) {
+          const uint32_t j = fj + rank;
+          const uint32_t s = np == (uint32_t)a.fused_p ? j >> a.fused_shift : j / np;
+          const uint32_t q = j - s * np;
+          int r, c;
+          item_ray_ls(a, seed, clp + q, s, st, p, d, r, c);
+          // the sample's LDS place: slot fst & 1, [pixel q][channel][sample s]
+          witem = (uint64_t)(q * 3u * (uint32_t)a.spp + s) | ((uint64_t)(fst & 1) << 31);
+          L = mk(0.f, 0.f, 0.f);
+          Le = L;
+          Ld = L;
+          M = mk(1.f, 1.f, 1.f);
+          k = 0;
+          active = true;
+        }
+        fj += (uint32_t)__popcll(need);
+        fj = fj < fn ? fj : fn;
+      }
+    } else if (need) {
       const uint32_t rank =
           __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
       if (!active) {
@@ -1011,7 +1100,14 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
 
     if (finished) {
       active = false;
-      if (MODE == MODE_FWD) {
+      if (MODE == MODE_FWDM) {
+        float *o = reinterpret_cast<float *>(reinterpret_cast<char *>(lds) + a.mean_off) +
+                   (size_t)(tid >> 6) * 2 * a.mean_slot + ((witem >> 31) ? a.mean_slot : 0u) +
+                   (uint32_t)(witem & 0x7fffffffu);
+        o[0] = L.x;
+        o[a.spp] = L.y;
+        o[2 * a.spp] = L.z;
+      } else if (MODE == MODE_FWD) {
         float *o = out_samples + witem * 3;
         o[0] = L.x;
         o[1] = L.y;
@@ -1111,6 +1207,55 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           rslot = 0;
           rhi = lo;
           active = true;
+        }
+      }
+    }
+    if (MODE == MODE_FWDM) {
+      // fused pixel mean: count the finished samples per slot; a slot whose
+      // last sample came in is summed now (toneMap, path_trace.cu:186-198:
+      // per pixel, per channel, v_s / spp added in sample order -- the same
+      // float operations as pixel_mean_sm_kernel) by lanes 3q + c, then freed
+      const uint64_t fm = __ballot(finished);
+      if (fm) {
+        const int n1 = __popcll(__ballot(finished && (witem >> 31) != 0));
+        const int n0 = __popcll(fm) - n1;
+        fl0 -= n0;
+        fl1 -= n1;
+        const bool red0 = n0 > 0 && fl0 == 0, red1 = n1 > 0 && fl1 == 0;
+        if (red0 || red1) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slot's sample writes before the sums
+          __builtin_amdgcn_wave_barrier();
+          const int spp = a.spp;
+          const lds_f32 *wbase = (const lds_f32 *)(reinterpret_cast<char *>(lds) + a.mean_off) +
+                                 (size_t)(tid >> 6) * 2 * a.mean_slot;
+          for (int x = 0; x < 2; ++x) {  // wave-uniform
+            if (!(x ? red1 : red0)) continue;
+            const uint64_t xleft = a.npix - (x ? f1lp : f0lp);
+            const int np = xleft < (uint64_t)a.fused_p ? (int)xleft : a.fused_p;
+            if (lane < 3 * np) {
+              const int q = (lane * 43) >> 7, ch = lane - 3 * q;  // lane / 3 for lane < 64
+              const lds_f32 *v = wbase + (x ? a.mean_slot : 0u) + (size_t)(3 * q + ch) * spp;
+              float acc = 0.f;
+              if (a.rc_spp != 0.f && (spp & 3) == 0) {  // x * (1/spp) == x / spp (power of two); 16-B reads
+                const float rc = a.rc_spp;
+                for (int s = 0; s < spp; s += 4) {
+                  const v4f w4 = *(const lds_v4 *)(v + s);
+                  acc += w4.x * rc;
+                  acc += w4.y * rc;
+                  acc += w4.z * rc;
+                  acc += w4.w * rc;
+                }
+              } else {
+                const float fs = (float)spp;
+                for (int s = 0; s < spp; ++s) acc += v[s] / fs;
+              }
+              const uint64_t px = (uint64_t)(x ? f1lp : f0lp) + (uint64_t)q;
+              out_samples[px * 3 + ch] = acc;
+              if (a.ldr) a.ldr[(size_t)set * a.out_stride + px * 3 + ch] = (uint8_t)(255.f * acc / (1 + acc));
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the sums' reads before the slot is refilled
+          __builtin_amdgcn_wave_barrier();
         }
       }
     }
@@ -1233,7 +1378,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
 #endif
   }
 
-  if (MODE != MODE_FWD) {
+  if (!is_fwd<MODE>()) {
     __syncthreads();
     if (n_acc > 0) {
       double *dstp = is_adj<MODE>() ? grad : edges;
@@ -1344,10 +1489,11 @@ struct GpuScene {
   uint32_t *big_pomask = nullptr;  // ... over the large-triangle pairs (BVH scenes)
   int accel = IPT_ACCEL_AUTO;
   int *grad_map = nullptr, *slot_tri = nullptr;  // ADJ hot-set LDS slots (large scenes)
-  int grid[16] = {0};       // resident workgroups per (mode, spec, bvh) (0 = not queried)
-  size_t grid_lds[16] = {0};
-  size_t pick_base[16] = {0};  // launch_bvh's LDS choice per (mode, spec): base bytes it was made for
-  int pick_opt[16] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+  int grid[20] = {0};       // resident workgroups per (mode, spec, bvh) (0 = not queried)
+  size_t grid_lds[20] = {0};
+  size_t pick_base[20] = {0};  // launch_bvh's LDS choice per (mode, spec): base bytes it was made for
+  size_t pick_tail[20] = {0};  // ... and the per-block tail (fused pixel mean slots) behind it
+  int pick_opt[20] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
   // dynamic-chunk counters per (stream, number of sets): zeroed once, then
   // advanced by every launch by a known amount (TraceArgs::chunk_base)
   struct Counters {
@@ -1617,6 +1763,12 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.rc_spp = (p.spp > 0 && p.spp <= (1 << 24) && (p.spp & (p.spp - 1)) == 0) ? 1.0f / (float)p.spp : 0.f;
   a.rc_W = (p.width > 0 && (p.width & (p.width - 1)) == 0) ? 1.0f / (float)p.width : 0.f;
   a.rc_H = (p.height > 0 && (p.height & (p.height - 1)) == 0) ? 1.0f / (float)p.height : 0.f;
+  a.fused = 0;
+  a.fused_p = 1;
+  a.fused_shift = 0;
+  a.mean_off = 0;
+  a.mean_slot = 0;
+  a.ldr = nullptr;
   return a;
 }
 
@@ -1738,8 +1890,13 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
     const uint64_t waves = (uint64_t)(a.nscenes > 1 ? b.bps : grid) * (kBlock / 64);
     uint64_t c = (a.n_samples / (waves * IPT_DYN_CHUNKS_PER_WAVE) + 63) / 64 * 64;
     c = std::min<uint64_t>(std::max<uint64_t>(c, IPT_DYN_MIN_CHUNK), 4096);
+    uint64_t units = a.n_samples;
+    if (a.fused) {  // fused pixel mean: chunks of fused_p pixels (all their samples)
+      c = (uint64_t)a.fused_p;
+      units = a.npix;
+    }
     b.chunk = (uint32_t)c;
-    const uint64_t chunks = (a.n_samples + c - 1) / c;
+    const uint64_t chunks = (units + c - 1) / c;
     const uint64_t grabs = (chunks > waves ? chunks - waves : 0) + waves;  // per set, see TraceArgs::chunk_base
     cap_ctr.st = st;
     if (stream_counters(s, st, a.nscenes, (uint32_t)grabs, &b.chunk_ctr, &b.chunk_base, &cap_ctr.p, &ctr_lock))
@@ -1770,15 +1927,15 @@ __global__ __launch_bounds__(kBlock) void kdpi_kernel(const float *__restrict__ 
 // bins sit just under 3 workgroups/CU, and the pair copy would tip it to 2
 // (6.6 -> 7.9 ms).  Cached per scene and instance for the base LDS bytes.
 template <int MODE, bool SPEC>
-static int launch_bvh_pick(GpuScene *s, TraceArgs &a, size_t *lds) {
+static int launch_bvh_pick(GpuScene *s, TraceArgs &a, size_t *lds, size_t tail) {
   const int slot = MODE * 4 + (SPEC ? 2 : 0);
   const bool opt[4][2] = {{true, true}, {true, false}, {false, true}, {false, false}};
   const size_t base = *lds;
-  if (s->pick_opt[slot] < 0 || s->pick_base[slot] != base) {
+  if (s->pick_opt[slot] < 0 || s->pick_base[slot] != base || s->pick_tail[slot] != tail) {
     int best = -1, best_per_cu = 0;
     for (int k = 0; k < 4; ++k) {
       TraceArgs b = a;
-      const size_t l = bvh_lds(s, b, base, opt[k][0], opt[k][1]);
+      const size_t l = bvh_lds_offset(bvh_lds(s, b, base, opt[k][0], opt[k][1])) + tail;
       if (l > 160 * 1024) continue;
       int per_cu = 0;
       HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<MODE, SPEC, true>,
@@ -1794,15 +1951,18 @@ static int launch_bvh_pick(GpuScene *s, TraceArgs &a, size_t *lds) {
     }
     s->pick_opt[slot] = best;
     s->pick_base[slot] = base;
+    s->pick_tail[slot] = tail;
   }
   const int k = s->pick_opt[slot];
   *lds = bvh_lds(s, a, base, opt[k][0], opt[k][1]);
   return 0;
 }
 
+// tail: bytes per workgroup placed after everything else (16-B aligned; the
+// fused pixel mean's sample slots, TraceArgs::mean_off).
 template <int MODE>
 static int launch(GpuScene *s, TraceArgs a, size_t lds, const float *kd_dev, float *out, const float *adj,
-                  double *grad, const uint8_t *target, double *edges, hipStream_t st) {
+                  double *grad, const uint8_t *target, double *edges, hipStream_t st, size_t tail = 0) {
   StreamScratch kdpi;
   if (MODE != MODE_GRAPH && !a.kd_tables && a.n_samples > 0) {
     const int n = 3 * s->host.nT * a.nscenes;
@@ -1822,14 +1982,23 @@ static int launch(GpuScene *s, TraceArgs a, size_t lds, const float *kd_dev, flo
       lds += ring;
     }
   }
+  auto add_tail = [&]() {
+    if (tail) {
+      a.mean_off = (uint32_t)bvh_lds_offset(lds);
+      lds = a.mean_off + tail;
+    }
+  };
   if (use_bvh(s)) {
     if (s->has_ks) {
-      if (launch_bvh_pick<MODE, true>(s, a, &lds)) return -1;
+      if (launch_bvh_pick<MODE, true>(s, a, &lds, tail)) return -1;
+      add_tail();
       return launch_inst<MODE, true, true>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
     }
-    if (launch_bvh_pick<MODE, false>(s, a, &lds)) return -1;
+    if (launch_bvh_pick<MODE, false>(s, a, &lds, tail)) return -1;
+    add_tail();
     return launch_inst<MODE, false, true>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
   }
+  add_tail();
   if (s->has_ks) return launch_inst<MODE, true, false>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
   return launch_inst<MODE, false, false>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
 }
@@ -1874,11 +2043,50 @@ int gpu_pixel_mean_sm(const float *samples_dev, int64_t npix, int spp, float *hd
   return pixel_mean_sm_sets(samples_dev, npix, spp, 1, hdr_dev, ldr_dev, stream);
 }
 
+// Fused pixel mean (IPT_FUSED_MEAN): pixels per chunk, or 0 when the launch
+// renders through the sample buffer + pixel_mean_sm_kernel instead.  A chunk
+// holds p pixels x spp samples with p * spp <= 256 (p a power of two <= 16,
+// so the 3p summing lanes fit a wave): two LDS slots of 3 KB at most per wave.
+// Bounded paths only (a path longer than a chunk's issue time stalls the
+// wave's refill until its slot is summed); the index math needs < 2^32
+// samples per frame.  IPT_RENDER_TWO_KERNEL=1 (environment) forces the
+// unfused path (A/B timing, tests).
+#ifndef IPT_FUSED_MEAN
+#define IPT_FUSED_MEAN 1
+#endif
+#ifndef IPT_FUSED_MAX_BOUNCES
+#define IPT_FUSED_MAX_BOUNCES 16
+#endif
+static int fused_pixels(const RenderParams &p) {
+  if (!IPT_FUSED_MEAN || !IPT_DYN_CHUNKS || std::getenv("IPT_RENDER_TWO_KERNEL")) return 0;
+  if (p.max_bounces < 0 || p.max_bounces > IPT_FUSED_MAX_BOUNCES || p.spp > 256) return 0;
+  if ((uint64_t)p.width * (uint64_t)p.height * (uint64_t)p.spp > 0xffffffffull) return 0;
+  int q = 1;
+  while (q < 16 && 2 * q * p.spp <= 256) q *= 2;
+  return q * p.spp >= 64 ? q : 0;
+}
+
 int gpu_render(GpuScene *s, const RenderParams &p, const float *kd_dev, float *hdr_dev, uint8_t *ldr_dev,
                void *stream) {
   if (check_params(s, p)) return -1;
   const int64_t npix = (int64_t)band_rows(p) * p.width;
   const int sets = p.nscenes > 1 ? p.nscenes : 1;
+  // BVH scenes keep the two-kernel render: their cooperative traversal wants
+  // the wave's rays spread over 64 pixels (a chunk's p <= 16 pixels put many
+  // lanes into the tree at once) and the slots cost the tree's LDS stage
+  // residency -- north-star 3.92 -> 4.60 ms fused (profiles/r03/fusedab_r03h.log)
+  if (const int fp = use_bvh(s) ? 0 : fused_pixels(p)) {
+    TraceArgs a = make_args(s, p);
+    a.fused = 1;
+    a.fused_p = fp;
+    while ((1 << a.fused_shift) < fp) ++a.fused_shift;
+    a.mean_slot = (uint32_t)(3 * fp * p.spp);
+    a.ldr = ldr_dev;
+    a.out_stride = (uint64_t)npix * 3;  // per material set: its own HDR (and LDR) image
+    const size_t tail = (size_t)(kBlock / 64) * 2 * a.mean_slot * sizeof(float);
+    return launch<MODE_FWDM>(s, a, table_bytes(a), kd_dev, hdr_dev, nullptr, nullptr, nullptr, nullptr,
+                             (hipStream_t)stream, tail);
+  }
   StreamScratch ws;
   if (ws.alloc((size_t)sets * npix * p.spp * 3 * sizeof(float), (hipStream_t)stream)) return -1;
   if (gpu_render_samples_sm(s, p, kd_dev, (float *)ws.p, stream)) return -1;

@@ -36,7 +36,8 @@ def main(fetch_dir, write_dir, out):
         kernels[k] = {"fetch_kb_raw": round(f_kb, 3), "write_kb_raw": round(w_kb, 3),
                       "hbm_bytes_per_launch": int(round(2 * f_kb * 1024 + w_kb * 1024)),
                       "launches": max(fe.get(k, (0, 0))[1], wr.get(k, (0, 0))[1])}
-    fwd = [k for k in kernels if "trace_kernel<0" in k]
+    # the forward of the headline: the fused render (MODE_FWDM = 4), else the unfused trace kernel
+    fwd = [k for k in kernels if "trace_kernel<4" in k] or [k for k in kernels if "trace_kernel<0" in k]
     res = {"source": [fetch_dir, write_dir], "correction": "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024",
            "kernels": kernels}
     if fwd:
