@@ -200,6 +200,10 @@ struct TraceArgs {
   // `wave` of `chunk` items and then takes chunk nwaves + atomicAdd(ctr[set])
   // until the launch's items are used up; chunk 0 = static per-wave ranges
   uint32_t chunk;
+  // guided sizes: the first chunk_big_n chunks hold `chunk` units, the rest
+  // chunk_small (units: work items, or pixels in MODE_FWDM), so a launch ends
+  // on small chunks and its waves run dry close together (chunk_range)
+  uint32_t chunk_small, chunk_big_n;
   uint32_t *chunk_ctr;
   // value of every set's counter when this launch starts: the counters are
   // never reset (no memset launch per launch) -- a launch grabs exactly
@@ -214,12 +218,12 @@ struct TraceArgs {
   // BVH scenes: the same masks over the large-triangle pairs (nullptr = none)
   const uint32_t *big_pomask;
   // FWD with the pixel mean fused in (gpu_render, IPT_FUSED_MEAN): work comes
-  // in chunks of fused_p (= 2^fused_shift) launch-local pixels x spp samples;
+  // in chunks of `chunk` (then chunk_small) launch-local pixels x spp samples;
   // a finished sample goes to its chunk's slot in the wave's LDS (two slots
   // per wave, mean_slot floats each, at byte mean_off of the dynamic LDS),
   // and when the last sample of a chunk is in, the wave sums each pixel's
   // samples in sample order (toneMap) into out_samples (HDR, npix x 3) and ldr
-  int fused, fused_p, fused_shift;
+  int fused;
   uint32_t mean_off, mean_slot;
   uint8_t *ldr;
 };
@@ -264,6 +268,30 @@ __device__ __forceinline__ void local_rc(const TraceArgs &a, uint64_t lp, int &r
     c = (int)(lp - lr * (uint64_t)a.W);
   }
   r = a.row0 + (int)lr * a.row_step;
+}
+
+// Chunk g of a launch (TraceArgs::chunk_big_n) -> units [start, end).
+// GUIDED: the BVH instances (guided_tail); the others take `chunk` units.
+template <bool GUIDED>
+__device__ __forceinline__ void chunk_range(const TraceArgs &a, uint64_t g, uint64_t units, uint64_t &start,
+                                            uint64_t &end) {
+  const uint64_t nb = a.chunk_big_n;
+  uint64_t len;
+  if (!GUIDED || g < nb) {
+    start = g * a.chunk;
+    len = a.chunk;
+  } else {
+    start = nb * a.chunk + (g - nb) * a.chunk_small;
+    len = a.chunk_small;
+  }
+  end = start + len < units ? start + len : units;
+}
+// MODE_FWDM: pixels of the chunk that starts at launch-local pixel lp
+template <bool GUIDED>
+__device__ __forceinline__ uint32_t fused_np(const TraceArgs &a, uint64_t lp) {
+  const uint64_t len = !GUIDED || lp < (uint64_t)a.chunk_big_n * a.chunk ? a.chunk : a.chunk_small;
+  const uint64_t left = a.npix - lp;
+  return (uint32_t)(left < len ? left : len);
 }
 
 // global pixel index (r * W + c) of this launch's work item w
@@ -615,8 +643,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   const bool dyn = a.chunk != 0;
   uint64_t next, end;
   if (dyn) {
-    next = (uint64_t)wave * a.chunk;
-    end = next + a.chunk < a.n_samples ? next + a.chunk : a.n_samples;
+    chunk_range<BVH>(a, wave, a.n_samples, next, end);
   } else {
     next = (a.n_samples * wave) / nwaves;
     end = (a.n_samples * (wave + 1)) / nwaves;
@@ -679,27 +706,24 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     if (MODE == MODE_FWDM) {
       // the current chunk is fully issued and the other slot is free: the
       // next chunk goes there (first the wave's own, then from the counter)
-      const uint32_t clp = (fst & 1) ? f1lp : f0lp;
-      const uint64_t cleft = a.npix - clp;
-      const uint32_t cn = (uint32_t)(cleft < (uint64_t)a.fused_p ? cleft : (uint64_t)a.fused_p) * (uint32_t)a.spp;
+      const uint32_t cn = fused_np<BVH>(a, (fst & 1) ? f1lp : f0lp) * (uint32_t)a.spp;
       if ((!(fst & 2) || fj >= cn) && !exhausted && ((fst & 1) ? fl0 : fl1) == 0) {
         // (a wave whose own chunk is past the end grabs once, as in the
         // unfused protocol: every wave's last grab fails, TraceArgs::chunk_base)
-        uint32_t blk = wave;
+        uint64_t lp0, lp1;
         bool own = false;
         if (!(fst & 2)) {
           fst |= 2;
-          own = ((uint64_t)blk << a.fused_shift) < a.npix;
+          chunk_range<BVH>(a, wave, a.npix, lp0, lp1);
+          own = lp0 < a.npix;
         }
         if (!own) {
           uint32_t c = 0;
           if (lane == 0) c = atomicAdd(a.chunk_ctr + set, 1u) - a.chunk_base;
-          blk = nwaves + (uint32_t)__builtin_amdgcn_readfirstlane((int)c);  // lane 0 (full exec here)
+          chunk_range<BVH>(a, nwaves + (uint32_t)__builtin_amdgcn_readfirstlane((int)c), a.npix, lp0, lp1);  // lane 0 (full exec here)
         }
-        const uint64_t lp0 = (uint64_t)blk << a.fused_shift;
         if (lp0 < a.npix) {
-          const uint64_t left = a.npix - lp0;
-          const int n = (left < (uint64_t)a.fused_p ? (int)left : a.fused_p) * a.spp;
+          const int n = (int)(lp1 - lp0) * a.spp;
           fst ^= 1;
           if (fst & 1) {
             f1lp = (uint32_t)lp0;
@@ -720,10 +744,11 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       uint32_t c = 0;
       if (lane == 0) c = atomicAdd(a.chunk_ctr + set, 1u) - a.chunk_base;
       c = (uint32_t)__shfl((int)c, 0);
-      const uint64_t start = (uint64_t)(nwaves + c) * a.chunk;
+      uint64_t start, stop;
+      chunk_range<BVH>(a, nwaves + c, a.n_samples, start, stop);
       if (start < a.n_samples) {
         next = start;
-        end = start + a.chunk < a.n_samples ? start + a.chunk : a.n_samples;
+        end = stop;
       } else {
         exhausted = true;
       }
@@ -784,15 +809,14 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     const uint64_t need = RING ? 0ull : __ballot(!active);
     if (MODE == MODE_FWDM) {
       const uint32_t clp = (fst & 1) ? f1lp : f0lp;
-      const uint64_t cleft = a.npix - clp;
-      const uint32_t np = (uint32_t)(cleft < (uint64_t)a.fused_p ? cleft : (uint64_t)a.fused_p);
+      const uint32_t np = fused_np<BVH>(a, clp);
       const uint32_t fn = np * (uint32_t)a.spp;
       if (need && (fst & 2) && fj < fn) {
         const uint32_t rank =
             __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
         if (!active && fj + rank < fn) {
           const uint32_t j = fj + rank;
-          const uint32_t s = np == (uint32_t)a.fused_p ? j >> a.fused_shift : j / np;
+          const uint32_t s = (np & (np - 1u)) == 0u ? j >> __builtin_ctz(np) : j / np;
           const uint32_t q = j - s * np;
           int r, c;
           item_ray_ls(a, seed, clp + q, s, st, p, d, r, c);
@@ -1230,8 +1254,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
                                  (size_t)(tid >> 6) * 2 * a.mean_slot;
           for (int x = 0; x < 2; ++x) {  // wave-uniform
             if (!(x ? red1 : red0)) continue;
-            const uint64_t xleft = a.npix - (x ? f1lp : f0lp);
-            const int np = xleft < (uint64_t)a.fused_p ? (int)xleft : a.fused_p;
+            const int np = (int)fused_np<BVH>(a, x ? f1lp : f0lp);
             if (lane < 3 * np) {
               const int q = (lane * 43) >> 7, ch = lane - 3 * q;  // lane / 3 for lane < 64
               const lds_f32 *v = wbase + (x ? a.mean_slot : 0u) + (size_t)(3 * q + ch) * spp;
@@ -1750,6 +1773,8 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.use_ring = 0;
   a.rec_cap = p.max_bounces >= 0 ? p.max_bounces + 1 : 0;
   a.chunk = 0;
+  a.chunk_small = 0;
+  a.chunk_big_n = 0;
   a.chunk_ctr = nullptr;
   a.chunk_base = 0;
   a.pboxes = s->pboxes;
@@ -1764,8 +1789,6 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.rc_W = (p.width > 0 && (p.width & (p.width - 1)) == 0) ? 1.0f / (float)p.width : 0.f;
   a.rc_H = (p.height > 0 && (p.height & (p.height - 1)) == 0) ? 1.0f / (float)p.height : 0.f;
   a.fused = 0;
-  a.fused_p = 1;
-  a.fused_shift = 0;
   a.mean_off = 0;
   a.mean_slot = 0;
   a.ldr = nullptr;
@@ -1865,6 +1888,29 @@ static int stream_counters(GpuScene *s, hipStream_t st, int sets, uint32_t grabs
   return 0;
 }
 
+// Guided chunk sizes (TraceArgs::chunk_big_n), BVH instances: a launch hands
+// out its last ~IPT_GUIDED_TAIL small chunks per wave (64 work items) after
+// the big ones, so the waves that take the last chunks finish close to the
+// others -- a BVH loop iteration is ~2.4x a brute-force one, so a big chunk
+// taken at the end kept its wave busy long after the rest of the grid ran
+// dry.  North-star 1/8 share: forward 0.814 -> 0.727 ms, adjoint 0.933 ->
+// 0.850 (4 per wave; 1 and 2 less).  The brute-force scenes lose with it
+// (C2 1/8 share 0.278 -> 0.297 ms at 2 per wave: the fused render's 64-sample
+// chunks outrun its two LDS slots, and each extra grab is an atomic round
+// trip the wave waits for), so their instances keep fixed chunks
+// (profiles/r03/envab_r03j.log).  The environment variable of the same name
+// overrides the count (A/B timing).
+#ifndef IPT_GUIDED_TAIL
+#define IPT_GUIDED_TAIL 4
+#endif
+#ifndef IPT_DYN_SMALL_CHUNK
+#define IPT_DYN_SMALL_CHUNK 64
+#endif
+static int guided_tail() {
+  const char *e = std::getenv("IPT_GUIDED_TAIL");
+  return e ? std::max(0, std::atoi(e)) : IPT_GUIDED_TAIL;
+}
+
 template <int MODE, bool SPEC, bool BVH>
 static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float *kd_dev, float *out, const float *adj,
                        double *grad, const uint8_t *target, double *edges, hipStream_t st) {
@@ -1890,13 +1936,19 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
     const uint64_t waves = (uint64_t)(a.nscenes > 1 ? b.bps : grid) * (kBlock / 64);
     uint64_t c = (a.n_samples / (waves * IPT_DYN_CHUNKS_PER_WAVE) + 63) / 64 * 64;
     c = std::min<uint64_t>(std::max<uint64_t>(c, IPT_DYN_MIN_CHUNK), 4096);
-    uint64_t units = a.n_samples;
-    if (a.fused) {  // fused pixel mean: chunks of fused_p pixels (all their samples)
-      c = (uint64_t)a.fused_p;
+    uint64_t units = a.n_samples, small = std::min<uint64_t>(c, IPT_DYN_SMALL_CHUNK);
+    if (a.fused) {  // fused pixel mean: chunks of a.chunk pixels (all their samples), small ones of >= 64 samples
+      c = a.chunk;
+      small = std::min<uint64_t>(c, std::max<uint64_t>(1, 64 / (uint64_t)a.spp));
       units = a.npix;
     }
+    // guided sizes: the last ~guided_tail() small chunks per wave end the launch
+    const uint64_t tail = BVH ? waves * (uint64_t)guided_tail() * small : 0;
+    const uint64_t nb = units > tail ? (units - tail) / c : 0;
     b.chunk = (uint32_t)c;
-    const uint64_t chunks = (units + c - 1) / c;
+    b.chunk_small = (uint32_t)small;
+    b.chunk_big_n = (uint32_t)nb;
+    const uint64_t chunks = nb + (units - nb * c + small - 1) / small;
     const uint64_t grabs = (chunks > waves ? chunks - waves : 0) + waves;  // per set, see TraceArgs::chunk_base
     cap_ctr.st = st;
     if (stream_counters(s, st, a.nscenes, (uint32_t)grabs, &b.chunk_ctr, &b.chunk_base, &cap_ctr.p, &ctr_lock))
@@ -2078,8 +2130,7 @@ int gpu_render(GpuScene *s, const RenderParams &p, const float *kd_dev, float *h
   if (const int fp = use_bvh(s) ? 0 : fused_pixels(p)) {
     TraceArgs a = make_args(s, p);
     a.fused = 1;
-    a.fused_p = fp;
-    while ((1 << a.fused_shift) < fp) ++a.fused_shift;
+    a.chunk = (uint32_t)fp;  // pixels per (big) chunk; launch_inst adds the small ones
     a.mean_slot = (uint32_t)(3 * fp * p.spp);
     a.ldr = ldr_dev;
     a.out_stride = (uint64_t)npix * 3;  // per material set: its own HDR (and LDR) image

@@ -24,7 +24,7 @@
 #   multirank    2-rank gloo rehearsal of bench.py on the one GPU
 #   scaling      tools/launch_scaling.py (fixed cost per launch: C2 shares 1/1 .. 1/64)
 #   workflow     tools/workflow_at_size.py (pipeline all --n 100 + optimize --n 100)
-#   fusedab      tools/fused_ab.py (fused pixel mean vs two-kernel render)
+#   envab        tools/env_ab.py $ENVAB (launch-time switches from the environment, A/B)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 R=$(pwd)
@@ -79,7 +79,7 @@ run() {
                    --warmup 4 > "$OUT/bench_2rank_$T.json" 2> "$OUT/bench_2rank_$T.err" ;;
     scaling) timeout -k 10 300 python tools/launch_scaling.py > "$OUT/scaling_$T.jsonl" 2> "$OUT/scaling_$T.err" ;;
     workflow) timeout -k 10 1000 python -u tools/workflow_at_size.py --out "$OUT/workflow_$T.json" > "$OUT/workflow_$T.log" 2>&1 ;;
-    fusedab) timeout -k 10 300 python tools/fused_ab.py > "$OUT/fusedab_$T.log" 2>&1 ;;
+    envab) timeout -k 10 400 python tools/env_ab.py ${ENVAB:-base:} > "$OUT/envab_$T.log" 2>&1 ;;
     *) echo "unknown stage $1" >&2; return 2 ;;
   esac
 }

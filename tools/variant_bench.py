@@ -95,7 +95,9 @@ def main():
         adj = torch.ones((512, 512, 3), device=dev)
         g = torch.zeros((8192, 3), dtype=torch.float64, device=dev)
         pb = N.make_params(512, 512, 64, 4, 0, 192, 256)  # one 64-row band: a small launch (the 8-GPU share)
-        kinds = ("fwd", "fsm", "adj", "band")
+        pr8 = N.make_params(512, 512, 64, 4, 0, 0, 512, 8)  # one interleaved 1/8 share (the bench's tile split)
+        hdr = torch.empty((512 * 512, 3), device=dev)
+        kinds = ("fwd", "fsm", "adj", "band", "render", "render8", "adj8")
         times = {n: {k: [] for k in kinds} for n in libs}
         for rnd in range(6):
             for n, L in libs.items():
@@ -111,6 +113,11 @@ def main():
                             assert L.ipt_render_samples_sm_dev(hs[n], C.byref(p), None, buf.data_ptr(), st) == 0
                         elif kind == "band":
                             assert L.ipt_render_samples_sm_dev(hs[n], C.byref(pb), None, buf.data_ptr(), st) == 0
+                        elif kind in ("render", "render8"):
+                            pp = p if kind == "render" else pr8
+                            assert L.ipt_render_dev(hs[n], C.byref(pp), None, hdr.data_ptr(), None, st) == 0
+                        elif kind == "adj8":
+                            assert L.ipt_adjoint_dev(hs[n], C.byref(pr8), None, adj.data_ptr(), g.data_ptr(), st) == 0
                         else:
                             assert L.ipt_adjoint_dev(hs[n], C.byref(p), None, adj.data_ptr(), g.data_ptr(), st) == 0
                     e1.record()
@@ -122,6 +129,9 @@ def main():
             fs = np.median(times[n]["fsm"]) if times[n]["fsm"] else float("nan")
             out[sname + ":" + n] = {"fwd_ms": round(f, 4), "fsm_ms": round(fs, 4), "adj_ms": round(a, 4),
                                     "band_ms": round(float(np.median(times[n]["band"])), 4),
+                                    "render_ms": round(float(np.median(times[n]["render"])), 4),
+                                    "render8_ms": round(float(np.median(times[n]["render8"])), 4),
+                                    "adj8_ms": round(float(np.median(times[n]["adj8"])), 4),
                                     "fwd_Msps": round(512 * 512 * 64 / f / 1e3, 1), "adj_Msps": round(512 * 512 * 64 / a / 1e3, 1)}
             print(sname, n, out[sname + ":" + n], flush=True)
     print(json.dumps(out))
