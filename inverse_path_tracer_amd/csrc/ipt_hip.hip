@@ -118,6 +118,8 @@ constexpr int kAdjuRing = IPT_ADJU_RING;
 #define IPT_DYN_MIN_CHUNK 128
 #endif
 constexpr int kMaxTableTris = 512;  // kd/kd-over-pi LDS tables up to 12 KB
+// (an LDS table of the emission Ke next to them -- vertex 0's Le, the
+// emitter's lo, the sweep's lo -- measured neutral, profiles/r03/variants_ke_ring_r03n.log)
 #ifndef IPT_LDS_GRAD_KB
 #define IPT_LDS_GRAD_KB 12
 #endif
@@ -391,11 +393,13 @@ constexpr int min_blocks() {
 #define IPT_GRAPH_LDS_KB 64
 #endif
 // IPT_RAY_RING=1: camera rays come from a per-wave LDS ring filled 64 at a
-// time (trace_kernel).  Brute-force adjoint only: C2 adjoint 3.01 -> 2.95 ms,
-// C3 3.93 -> 3.87 (profiles/r01_variants_ray_ring.log); the BVH instances'
-// LDS is spoken for; the graph also needs the target pixel.
+// time (trace_kernel).  Brute-force adjoint only: C2 adjoint 3.01 -> 2.95 ms
+// in round 1 (profiles/r01_variants_ray_ring.log), neutral in round 2, and
+// 3% slower (C2 2.10 vs 2.16 ms, scenes/0 2.51 vs 2.59 without it) in round
+// 3 once the sweep's scan cut the per-path cost (profiles/r03/variants_sweep_r03m.log):
+// off, its 9 KB per workgroup left to the tables.
 #ifndef IPT_RAY_RING
-#define IPT_RAY_RING 1
+#define IPT_RAY_RING 0
 #endif
 constexpr int kRingFields = 9;  // d.xyz, XORWOW d, v0..v4
 template <int MODE, bool BVH>
@@ -465,6 +469,39 @@ __device__ __forceinline__ float *big_lds_copy(const TraceArgs &a, float *at, fl
   return at + big_lds_bytes(a.bvh_nbig) / sizeof(float);
 }
 
+// Wave-wide inclusive scans (GFX9 DPP: row_shr 1..8 inside each 16-lane
+// row, then row_bcast:15 / row_bcast:31 carry the rows' totals; lanes a
+// stage does not write add / max the identity 0).
+// IPT_SWEEP_SCAN=1: the adjoint sweep's task scan and owner search use them
+// (an LDS scatter of owner markers + a max-scan) instead of six dependent
+// ds_bpermute steps each.
+#ifndef IPT_SWEEP_SCAN
+#define IPT_SWEEP_SCAN 1
+#endif
+template <int CTRL, int ROW, int BANK>
+__device__ __forceinline__ int dpp0(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROW, BANK, true);
+}
+__device__ __forceinline__ int wave_scan_add(int v) {
+  int s = v + dpp0<0x111, 0xf, 0xf>(v);
+  s += dpp0<0x112, 0xf, 0xf>(v);
+  s += dpp0<0x113, 0xf, 0xf>(v);
+  s += dpp0<0x114, 0xf, 0xe>(s);
+  s += dpp0<0x118, 0xf, 0xc>(s);
+  s += dpp0<0x142, 0xa, 0xf>(s);
+  s += dpp0<0x143, 0xc, 0xf>(s);
+  return s;
+}
+__device__ __forceinline__ uint32_t wave_scan_max(uint32_t v) {
+  v = max(v, (uint32_t)dpp0<0x111, 0xf, 0xf>((int)v));
+  v = max(v, (uint32_t)dpp0<0x112, 0xf, 0xf>((int)v));
+  v = max(v, (uint32_t)dpp0<0x114, 0xf, 0xf>((int)v));
+  v = max(v, (uint32_t)dpp0<0x118, 0xf, 0xf>((int)v));
+  v = max(v, (uint32_t)dpp0<0x142, 0xa, 0xf>((int)v));
+  v = max(v, (uint32_t)dpp0<0x143, 0xc, 0xf>((int)v));
+  return v;
+}
+
 // TraceArgs is the kernel's FIRST parameter, so it sits at offset 0 of the
 // kernarg segment -- the in-loop reload below depends on that (IPT_ARGS_RELOAD).
 template <int MODE, bool SPEC, bool BVH>
@@ -522,6 +559,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     if (a.kd_tables) return mk(tab_l[3 * t], tab_l[3 * t + 1], tab_l[3 * t + 2]);
     return mk(kd_g[3 * t], kd_g[3 * t + 1], kd_g[3 * t + 2]);
   };
+  auto ke3 = [&](int t) -> V3 {  // TriMat::ke
+    const gbl_f32 *q = (const gbl_f32 *)mat + (size_t)t * (sizeof(TriMat) / sizeof(float)) + offsetof(TriMat, ke) / sizeof(float);
+    return mk(q[0], q[1], q[2]);
+  };
   auto kdpi3 = [&](int t) -> V3 {
     if (a.kd_tables) return mk(tab_l[3 * nT + 3 * t], tab_l[3 * nT + 3 * t + 1], tab_l[3 * nT + 3 * t + 2]);
     const gbl_f32 *q = (const gbl_f32 *)kdpi_g + 3 * t;
@@ -557,6 +598,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   if (po)
     for (int i = tid; i < nT * nE; i += nthr) lds_po[i] = a.pomask[i];
   float *lds_rec = a.small_pairs ? reinterpret_cast<float *>(lds_po) + (po ? nT * nE : 0) : lds_e3;
+  // MODE_ADJ with IPT_SWEEP_SCAN: one word per lane (the sweep's owner
+  // markers) in front of the vertex records
+  if (MODE == MODE_ADJ && IPT_SWEEP_SCAN) lds_rec += kBlock;
   // Camera-ray ring (RING instances): per wave kRingFields x 64 words after the
   // ADJ records, then the camera origin (3 floats per wave).
   const bool RING = ring_on<MODE, BVH>() && a.use_ring;
@@ -911,8 +955,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         const size_t bin = (size_t)dst * nT + tri;
         bins_add(a.lds_edges != 0, edges, a.lds_edges ? bin * kEdgeL : bin * kEdgeW, 5, v);
       } else if (k == 0) {
-        const TriMat &m = mat[tri];
-        Le = mk(m.ke[0], m.ke[1], m.ke[2]);
+        Le = ke3(tri);
       }
       nh = shading_normal(geom[tri], q);
       p = q;
@@ -1043,7 +1086,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
               s64 = q / (double)emit_pmf[emitter];
             const float s = (float)s64;
 #endif
-            lo = mk(me.ke[0] * s, me.ke[1] * s, me.ke[2] * s);
+            const V3 kee = ke3(et);
+            lo = mk(kee.x * s, kee.y * s, kee.z * s);
             emit_s = s;
             emit_et = et;
             const TriMat &m = mat[tri];
@@ -1157,8 +1201,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             return lds_rec + (size_t)sl * kBlock + tid;
           };
           auto rec_lo = [&](const float *r) {  // the forward's lo, same products
-            const TriMat &me = mat[__float_as_uint(r[0]) >> 16];
-            return mk(me.ke[0] * r[fs], me.ke[1] * r[fs], me.ke[2] * r[fs]);
+            const V3 kee = ke3((int)(__float_as_uint(r[0]) >> 16));
+            return mk(kee.x * r[fs], kee.y * r[fs], kee.z * r[fs]);
           };
           auto tdiff = [&](const float *r) {  // T_j = kd/pi (+ Ks*speci)
             const int tj = (int)(__float_as_uint(r[0]) & 0xffffu);
@@ -1301,12 +1345,19 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       if (__ballot(Kf > 0)) {
 #endif
         const int lane = tid & 63;
+#if IPT_SWEEP_SCAN
+        const int inc = wave_scan_add(Kf);  // inclusive scan of the task counts over the wave
+        const int T = __builtin_amdgcn_readlane(inc, 63);
+        // per-wave LDS word per lane: the round's owner markers
+        uint32_t *swl = reinterpret_cast<uint32_t *>(lds_rec) - kBlock + (tid & ~63);
+#else
         int inc = Kf;  // inclusive scan of the task counts over the wave
         for (int dd = 1; dd < 64; dd <<= 1) {
           const int y = __shfl_up(inc, dd);
           if (lane >= dd) inc += y;
         }
         const int T = __shfl(inc, 63);
+#endif
         float wx = 0.f, wy = 0.f, wz = 0.f;  // the owner's adjoint weights dL/dI / spp
         if (Kf > 0) {
           const uint64_t pixel = item_pixel(a, witem);
@@ -1325,31 +1376,65 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         while (base < T) {  // wave-uniform
           // this round: the whole paths whose tasks end by base + 64
           const uint64_t fit = __ballot(Kf > 0 && inc <= base + 64);
+#if IPT_SWEEP_SCAN
+          const int next = __builtin_amdgcn_readlane(inc, 63 - (int)__builtin_clzll(fit));
+          const int t = base + lane;
+          const bool valid = t < next;
+          // owners of this round mark their first task's lane with (start,
+          // escaped, K, owner lane) + 1 -- start in the top bits, so an
+          // inclusive max-scan leaves every task lane the marker of the last
+          // owner starting at or before it: its own path
+          swl[lane] = 0u;
+          const int st0 = inc - Kf - base;
+          if (Kf > 0 && inc <= next && st0 >= 0)
+            swl[st0] = (((uint32_t)st0 << 13) | (escaped ? 1u << 12 : 0u) | ((uint32_t)Kf << 6) | (uint32_t)lane) + 1u;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          const uint32_t mk_ = wave_scan_max(swl[lane]) - 1u;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // read before the next round's marks
+          __builtin_amdgcn_wave_barrier();
+          const int ow = valid ? (int)(mk_ & 63u) : lane;
+          const int KL = valid ? (int)((mk_ >> 6) & 63u) : 0;
+          const int kk = valid ? lane - (int)(mk_ >> 13) : 0;
+          const bool esc_o = valid && ((mk_ >> 12) & 1u);
+#else
           const int next = __shfl(inc, 63 - (int)__builtin_clzll(fit));
           const int t = base + lane;
           const bool valid = t < next;
           int ow = 0;  // owner lane: the smallest with inc > t
+#ifdef IPT_ABL_SWP_NOOWNER  // timing-only ablation builds of the sweep's parts (wrong gradients)
+          ow = lane;
+#else
           for (int step = 32; step >= 1; step >>= 1)
             if (__shfl(inc, ow + step - 1) <= t) ow += step;
+#endif
           // every shuffle reads a lane that may not hold a task of this
           // round, so all of them run with the whole wave active (a
           // ds_bpermute from an inactive lane returns 0)
           const int KL = __shfl(Kf, ow);
           const int inco = __shfl(inc, ow);
           const int kk = valid ? t - (inco - KL) : 0;
+          const bool esc_o = __shfl(escaped ? 1 : 0, ow) != 0;
+#endif
           const int rr = valid ? KL - 1 - kk : 0;  // vertices after this one
-          const bool esc = __shfl(escaped ? 1 : 0, ow) != 0;
+#ifdef IPT_ABL_SWP_NOOWNDATA
+          const bool esc = escaped;
+          const float ax = wx, ay = wy, az = wz;
+          const V3 LeL = Le, ML = M;
+#else
+          const bool esc = esc_o;
           const float ax = __shfl(wx, ow), ay = __shfl(wy, ow), az = __shfl(wz, ow);
           const V3 LeL = mk(__shfl(Le.x, ow), __shfl(Le.y, ow), __shfl(Le.z, ow));
           const V3 ML = mk(__shfl(M.x, ow), __shfl(M.y, ow), __shfl(M.z, ow));
+#endif
           // this task's record (lanes past the round read vertex 0 of a valid column)
           const float *r = lds_rec + (tid & ~63) + (valid ? ow : lane) + (size_t)kk * kBlock;
           const uint32_t f0 = valid ? __float_as_uint(r[0]) : 0u;
           const float es = r[fs], ck = r[2 * fs];
           // (the min()s keep a mis-indexed record from reaching global memory out of bounds)
           const int tk = min((int)(f0 & 0xffffu), nT - 1);
-          const TriMat &me = mat[min((int)(f0 >> 16), nT - 1)];
-          const V3 lk = mk(me.ke[0] * es, me.ke[1] * es, me.ke[2] * es);  // the forward's lo, same products
+          const V3 kee = ke3(min((int)(f0 >> 16), nT - 1));
+          const V3 lk = mk(kee.x * es, kee.y * es, kee.z * es);  // the forward's lo, same products
           V3 dj = kd3(tk), tv = kdpi3(tk);  // D = kd (+ Ks*specd), T = kd/pi (+ Ks*speci)
           if (SPEC) {
             const TriMat &mj = mat[tk];
@@ -1359,20 +1444,24 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           }
           // prefix: M_0 = 1, M_s = (M_{s-1} * T_{s-1}) * c_{s-1} from the left neighbour
           V3 Mk = mk(1.f, 1.f, 1.f);
+#ifndef IPT_ABL_SWP_NOPREFIX
           for (int s = 1; __ballot(valid && kk >= s); ++s) {
             const V3 N = mk((Mk.x * tv.x) * ck, (Mk.y * tv.y) * ck, (Mk.z * tv.z) * ck);
             const V3 Nl = mk(wave_shr1(N.x), wave_shr1(N.y), wave_shr1(N.z));
             if (kk == s) Mk = Nl;
           }
+#endif
           // suffix: S_K = escaped ? Le + D_{K-1} lo_{K-1} : 0, S_j = (Le + D_j lo_j) + (T_j c_j) S_{j+1}
           const V3 A = mk(LeL.x + dj.x * lk.x, LeL.y + dj.y * lk.y, LeL.z + dj.z * lk.z);
           const V3 B = mk(tv.x * ck, tv.y * ck, tv.z * ck);
           V3 S = (esc && rr == 0) ? A : mk(0.f, 0.f, 0.f);
+#ifndef IPT_ABL_SWP_NOSUFFIX
           for (int s = 1; __ballot(valid && rr >= s); ++s) {
             const V3 H = mk(A.x + B.x * S.x, A.y + B.y * S.y, A.z + B.z * S.z);
             const V3 Hr = mk(wave_shl1(H.x), wave_shl1(H.y), wave_shl1(H.z));
             if (rr == s) S = Hr;
           }
+#endif
           if (valid) {
             V3 dLd = Mk;
             if (esc && rr == 0) dLd = mk(dLd.x + ML.x, dLd.y + ML.y, dLd.z + ML.z);
@@ -1417,7 +1506,11 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             j = (dst * nT + emit_tri[ie]) * kEdgeW + kEdgeL + q % 3;
           }
         }
+#ifndef IPT_ABL_NOFLUSH  // timing-only ablation build: bins never leave LDS
         if (v != 0.0) atomicAdd(dstp + j, v);
+#else
+        if (v == 12345.0) dstp[j] = v;
+#endif
       }
     }
   }
@@ -2167,6 +2260,7 @@ int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const f
   }
   if (unbounded) a.rec_cap = kAdjuRing;
   const size_t lds = (size_t)a.grad_slots * 3 * sizeof(double) + table_bytes(a) +
+                     (!unbounded && IPT_SWEEP_SCAN ? (size_t)kBlock * sizeof(uint32_t) : 0) +
                      (size_t)a.rec_cap * (s->has_ks ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock * sizeof(float);
   if (lds > 160 * 1024) {
     gpu_set_error("adjoint LDS footprint exceeds 160 KiB; lower max_bounces");
