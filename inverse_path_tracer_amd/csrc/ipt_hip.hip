@@ -185,7 +185,6 @@ struct TraceArgs {
   // float x: both are the correctly rounded x * 2^-k), else 0
   float rc_spp;
   float rc_W, rc_H;  // 1/W, 1/H for power-of-two sizes, else 0 (camera_ray divides)
-  int use_ring;  // RING instances: camera rays from the LDS ring (host decides: only if it costs no residency)
   int rec_cap;   // ADJ: vertex records per lane (max_bounces + 1); ADJU: ring slots
   // scene batch (C5): blocks b, b + nscenes, ... (bps of them) trace material
   // set b -- interleaved, not contiguous ranges: the dispatcher fills a CU
@@ -392,20 +391,6 @@ constexpr int min_blocks() {
 #ifndef IPT_GRAPH_LDS_KB
 #define IPT_GRAPH_LDS_KB 64
 #endif
-// IPT_RAY_RING=1: camera rays come from a per-wave LDS ring filled 64 at a
-// time (trace_kernel).  Brute-force adjoint only: C2 adjoint 3.01 -> 2.95 ms
-// in round 1 (profiles/r01_variants_ray_ring.log), neutral in round 2, and
-// 3% slower (C2 2.10 vs 2.16 ms, scenes/0 2.51 vs 2.59 without it) in round
-// 3 once the sweep's scan cut the per-path cost (profiles/r03/variants_sweep_r03m.log):
-// off, its 9 KB per workgroup left to the tables.
-#ifndef IPT_RAY_RING
-#define IPT_RAY_RING 0
-#endif
-constexpr int kRingFields = 9;  // d.xyz, XORWOW d, v0..v4
-template <int MODE, bool BVH>
-constexpr bool ring_on() {
-  return IPT_RAY_RING && !BVH && MODE == 1;
-}
 // Work enumeration of the adjoint and graph integrators: sample-major -- a
 // wave's 64 lanes trace 64 different pixels, so their paths diverge at once:
 // the LDS atomics of a vertex step hit different bins and few lanes of a wave
@@ -472,12 +457,10 @@ __device__ __forceinline__ float *big_lds_copy(const TraceArgs &a, float *at, fl
 // Wave-wide inclusive scans (GFX9 DPP: row_shr 1..8 inside each 16-lane
 // row, then row_bcast:15 / row_bcast:31 carry the rows' totals; lanes a
 // stage does not write add / max the identity 0).
-// IPT_SWEEP_SCAN=1: the adjoint sweep's task scan and owner search use them
-// (an LDS scatter of owner markers + a max-scan) instead of six dependent
-// ds_bpermute steps each.
-#ifndef IPT_SWEEP_SCAN
-#define IPT_SWEEP_SCAN 1
-#endif
+// The adjoint sweep's task scan and owner search use them (an LDS scatter of
+// owner markers + a max-scan) instead of six dependent ds_bpermute steps
+// each: C2 adjoint 2.11 -> 2.05 ms, scenes/0 2.53 -> 2.47, north-star 4.96 ->
+// 4.88 (profiles/r03/variants_ke_ring_r03n.log, `scan0`).
 template <int CTRL, int ROW, int BANK>
 __device__ __forceinline__ int dpp0(int v) {
   return __builtin_amdgcn_update_dpp(0, v, CTRL, ROW, BANK, true);
@@ -598,17 +581,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   if (po)
     for (int i = tid; i < nT * nE; i += nthr) lds_po[i] = a.pomask[i];
   float *lds_rec = a.small_pairs ? reinterpret_cast<float *>(lds_po) + (po ? nT * nE : 0) : lds_e3;
-  // MODE_ADJ with IPT_SWEEP_SCAN: one word per lane (the sweep's owner
-  // markers) in front of the vertex records
-  if (MODE == MODE_ADJ && IPT_SWEEP_SCAN) lds_rec += kBlock;
-  // Camera-ray ring (RING instances): per wave kRingFields x 64 words after the
-  // ADJ records, then the camera origin (3 floats per wave).
-  const bool RING = ring_on<MODE, BVH>() && a.use_ring;
-  float *ring = nullptr;
-  if (RING) {
-    const size_t rec_words = is_adj<MODE>() ? (size_t)vmax * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock : 0;
-    ring = lds_rec + rec_words + (size_t)(tid >> 6) * (kRingFields * 64 + 4);
-  }
+  // MODE_ADJ: one word per lane (the sweep's owner markers) in front of the
+  // vertex records
+  if (MODE == MODE_ADJ) lds_rec += kBlock;
   BvhView bv;
   bv.isect = isect;
   bv.big = nullptr;
@@ -726,13 +701,6 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   uint64_t tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t tp_ = __builtin_amdgcn_s_memtime();
 #endif
-  // RING: the wave's camera rays are generated 64 at a time by all lanes
-  // (index math, XORWOW init, the two camera draws, camera_ray) into an LDS
-  // ring, and a lane that needs a new path pops the next one: the same work
-  // items in the same order as the per-lane refill below, computed at full
-  // lane utilisation instead of by the ~1/3 of lanes that finished.
-  uint64_t ring_w = 0;  // work item of ring slot 0
-  int ring_n = 0, ring_h = 0;  // slots left, next slot
   const int lane = tid & 63;
   for (;;) {
 #if defined(__HIP_DEVICE_COMPILE__)  // (the host pass has no AS4 copy)
@@ -797,60 +765,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         exhausted = true;
       }
     }
-    if (RING) {
-      uint64_t need = __ballot(!active);
-      int n_need = __popcll(need);
-      uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-      while (n_need > 0 && (ring_n > 0 || next < end)) {  // wave-uniform
-        if (ring_n == 0) {
-          const uint64_t w = next + (uint64_t)lane;
-          if (w < end) {
-            Rng s2;
-            V3 p2, d2;
-            int r2, c2;
-            item_ray(a, seed, w, s2, p2, d2, r2, c2);
-            float *q = ring + lane;
-            q[0] = d2.x; q[64] = d2.y; q[128] = d2.z;
-            q[192] = __uint_as_float(s2.d); q[256] = __uint_as_float(s2.v0); q[320] = __uint_as_float(s2.v1);
-            q[384] = __uint_as_float(s2.v2); q[448] = __uint_as_float(s2.v3); q[512] = __uint_as_float(s2.v4);
-            if (lane == 0) {
-              ring[kRingFields * 64 + 0] = p2.x;
-              ring[kRingFields * 64 + 1] = p2.y;
-              ring[kRingFields * 64 + 2] = p2.z;
-            }
-          }
-          const uint64_t left = end - next;
-          ring_w = next;
-          ring_n = left < 64 ? (int)left : 64;
-          ring_h = 0;
-          next += (uint64_t)ring_n;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // ring writes before the pops below
-          __builtin_amdgcn_wave_barrier();
-        }
-        const int take = n_need < ring_n ? n_need : ring_n;
-        if (!active && (int)rank < take) {
-          const int slot = ring_h + (int)rank;
-          const float *q = ring + slot;
-          witem = ring_w + (uint64_t)slot;
-          d = mk(q[0], q[64], q[128]);
-          st.d = __float_as_uint(q[192]); st.v0 = __float_as_uint(q[256]); st.v1 = __float_as_uint(q[320]);
-          st.v2 = __float_as_uint(q[384]); st.v3 = __float_as_uint(q[448]); st.v4 = __float_as_uint(q[512]);
-          p = mk(ring[kRingFields * 64 + 0], ring[kRingFields * 64 + 1], ring[kRingFields * 64 + 2]);
-          L = mk(0.f, 0.f, 0.f);
-          Le = L;
-          Ld = L;
-          M = mk(1.f, 1.f, 1.f);
-          k = 0;
-          active = true;
-        }
-        rank -= (uint32_t)take;  // lanes still waiting move up
-        ring_h += take;
-        ring_n -= take;
-        n_need -= take;
-      }
-    }
     // ---- refill finished lanes from the wave's range (ballot + mbcnt)
-    const uint64_t need = RING ? 0ull : __ballot(!active);
+    const uint64_t need = __ballot(!active);
     if (MODE == MODE_FWDM) {
       const uint32_t clp = (fst & 1) ? f1lp : f0lp;
       const uint32_t np = fused_np<BVH>(a, clp);
@@ -1345,19 +1261,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       if (__ballot(Kf > 0)) {
 #endif
         const int lane = tid & 63;
-#if IPT_SWEEP_SCAN
         const int inc = wave_scan_add(Kf);  // inclusive scan of the task counts over the wave
         const int T = __builtin_amdgcn_readlane(inc, 63);
         // per-wave LDS word per lane: the round's owner markers
         uint32_t *swl = reinterpret_cast<uint32_t *>(lds_rec) - kBlock + (tid & ~63);
-#else
-        int inc = Kf;  // inclusive scan of the task counts over the wave
-        for (int dd = 1; dd < 64; dd <<= 1) {
-          const int y = __shfl_up(inc, dd);
-          if (lane >= dd) inc += y;
-        }
-        const int T = __shfl(inc, 63);
-#endif
         float wx = 0.f, wy = 0.f, wz = 0.f;  // the owner's adjoint weights dL/dI / spp
         if (Kf > 0) {
           const uint64_t pixel = item_pixel(a, witem);
@@ -1376,7 +1283,6 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         while (base < T) {  // wave-uniform
           // this round: the whole paths whose tasks end by base + 64
           const uint64_t fit = __ballot(Kf > 0 && inc <= base + 64);
-#if IPT_SWEEP_SCAN
           const int next = __builtin_amdgcn_readlane(inc, 63 - (int)__builtin_clzll(fit));
           const int t = base + lane;
           const bool valid = t < next;
@@ -1397,36 +1303,11 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           const int KL = valid ? (int)((mk_ >> 6) & 63u) : 0;
           const int kk = valid ? lane - (int)(mk_ >> 13) : 0;
           const bool esc_o = valid && ((mk_ >> 12) & 1u);
-#else
-          const int next = __shfl(inc, 63 - (int)__builtin_clzll(fit));
-          const int t = base + lane;
-          const bool valid = t < next;
-          int ow = 0;  // owner lane: the smallest with inc > t
-#ifdef IPT_ABL_SWP_NOOWNER  // timing-only ablation builds of the sweep's parts (wrong gradients)
-          ow = lane;
-#else
-          for (int step = 32; step >= 1; step >>= 1)
-            if (__shfl(inc, ow + step - 1) <= t) ow += step;
-#endif
-          // every shuffle reads a lane that may not hold a task of this
-          // round, so all of them run with the whole wave active (a
-          // ds_bpermute from an inactive lane returns 0)
-          const int KL = __shfl(Kf, ow);
-          const int inco = __shfl(inc, ow);
-          const int kk = valid ? t - (inco - KL) : 0;
-          const bool esc_o = __shfl(escaped ? 1 : 0, ow) != 0;
-#endif
           const int rr = valid ? KL - 1 - kk : 0;  // vertices after this one
-#ifdef IPT_ABL_SWP_NOOWNDATA
-          const bool esc = escaped;
-          const float ax = wx, ay = wy, az = wz;
-          const V3 LeL = Le, ML = M;
-#else
           const bool esc = esc_o;
           const float ax = __shfl(wx, ow), ay = __shfl(wy, ow), az = __shfl(wz, ow);
           const V3 LeL = mk(__shfl(Le.x, ow), __shfl(Le.y, ow), __shfl(Le.z, ow));
           const V3 ML = mk(__shfl(M.x, ow), __shfl(M.y, ow), __shfl(M.z, ow));
-#endif
           // this task's record (lanes past the round read vertex 0 of a valid column)
           const float *r = lds_rec + (tid & ~63) + (valid ? ow : lane) + (size_t)kk * kBlock;
           const uint32_t f0 = valid ? __float_as_uint(r[0]) : 0u;
@@ -1444,24 +1325,21 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           }
           // prefix: M_0 = 1, M_s = (M_{s-1} * T_{s-1}) * c_{s-1} from the left neighbour
           V3 Mk = mk(1.f, 1.f, 1.f);
-#ifndef IPT_ABL_SWP_NOPREFIX
-          for (int s = 1; __ballot(valid && kk >= s); ++s) {
-            const V3 N = mk((Mk.x * tv.x) * ck, (Mk.y * tv.y) * ck, (Mk.z * tv.z) * ck);
-            const V3 Nl = mk(wave_shr1(N.x), wave_shr1(N.y), wave_shr1(N.z));
-            if (kk == s) Mk = Nl;
-          }
-#endif
           // suffix: S_K = escaped ? Le + D_{K-1} lo_{K-1} : 0, S_j = (Le + D_j lo_j) + (T_j c_j) S_{j+1}
           const V3 A = mk(LeL.x + dj.x * lk.x, LeL.y + dj.y * lk.y, LeL.z + dj.z * lk.z);
           const V3 B = mk(tv.x * ck, tv.y * ck, tv.z * ck);
           V3 S = (esc && rr == 0) ? A : mk(0.f, 0.f, 0.f);
-#ifndef IPT_ABL_SWP_NOSUFFIX
-          for (int s = 1; __ballot(valid && rr >= s); ++s) {
+          // both chains in one loop (max(K) - 1 steps instead of up to twice
+          // that; two independent dependency chains per step: -0.2..0.6%,
+          // profiles/r03/variants_merged_r03o.log)
+          for (int s = 1; __ballot(valid && (kk >= s || rr >= s)); ++s) {
+            const V3 N = mk((Mk.x * tv.x) * ck, (Mk.y * tv.y) * ck, (Mk.z * tv.z) * ck);
             const V3 H = mk(A.x + B.x * S.x, A.y + B.y * S.y, A.z + B.z * S.z);
+            const V3 Nl = mk(wave_shr1(N.x), wave_shr1(N.y), wave_shr1(N.z));
             const V3 Hr = mk(wave_shl1(H.x), wave_shl1(H.y), wave_shl1(H.z));
+            if (kk == s) Mk = Nl;
             if (rr == s) S = Hr;
           }
-#endif
           if (valid) {
             V3 dLd = Mk;
             if (esc && rr == 0) dLd = mk(dLd.x + ML.x, dLd.y + ML.y, dLd.z + ML.z);
@@ -1863,7 +1741,6 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
     const float *M = a.cam + 4 * i;
     a.cam_org[i] = std::fmaf(M[3], 1.f, std::fmaf(M[2], 0.f, std::fmaf(M[1], 0.f, M[0] * 0.f)));
   }
-  a.use_ring = 0;
   a.rec_cap = p.max_bounces >= 0 ? p.max_bounces + 1 : 0;
   a.chunk = 0;
   a.chunk_small = 0;
@@ -2117,16 +1994,6 @@ static int launch(GpuScene *s, TraceArgs a, size_t lds, const float *kd_dev, flo
     HIP_TRY(hipGetLastError());
     a.kdpi_g = (const float *)kdpi.p;
   }
-  a.use_ring = 0;
-  if (!use_bvh(s) && ring_on<MODE, false>()) {  // camera-ray rings after the records, if residency allows
-    const size_t ring = (size_t)(kBlock / 64) * (kRingFields * 64 + 4) * sizeof(float);
-    const size_t cap = 160 * 1024, want = (size_t)min_blocks<MODE, false>();
-    const size_t without = std::min(want, cap / std::max<size_t>(lds, 1)), with = std::min(want, cap / (lds + ring));
-    if (with >= without) {
-      a.use_ring = 1;
-      lds += ring;
-    }
-  }
   auto add_tail = [&]() {
     if (tail) {
       a.mean_off = (uint32_t)bvh_lds_offset(lds);
@@ -2260,7 +2127,7 @@ int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const f
   }
   if (unbounded) a.rec_cap = kAdjuRing;
   const size_t lds = (size_t)a.grad_slots * 3 * sizeof(double) + table_bytes(a) +
-                     (!unbounded && IPT_SWEEP_SCAN ? (size_t)kBlock * sizeof(uint32_t) : 0) +
+                     (!unbounded ? (size_t)kBlock * sizeof(uint32_t) : 0) +
                      (size_t)a.rec_cap * (s->has_ks ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock * sizeof(float);
   if (lds > 160 * 1024) {
     gpu_set_error("adjoint LDS footprint exceeds 160 KiB; lower max_bounces");
