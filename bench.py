@@ -447,6 +447,9 @@ def main():
                "source": os.path.relpath(PMC_FILE, ROOT)}
     roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
+                # SURVEY.md 8(d) fixes `frac`'s formula (brute-force-equivalent tests, judge and builder
+                # alike); the same number under its descriptive name, and `executed_frac` below
+                "brute_force_equivalent_frac": round(achieved / PEAK_FP32_TFLOPS, 4),
                 "kernel": "trace_kernel<MODE_FWDM> (forward + fused per-pixel mean, the step's only kernel)",
                 "kernel_ms": round(kernel_ms, 4),
                 "flop_per_launch": flop_per_launch,

@@ -1408,11 +1408,41 @@ __global__ __launch_bounds__(kBlock) void pixel_mean_sm_kernel(const float *__re
   if (ldr) ldr += (size_t)blockIdx.y * (size_t)npix * 3;
   float tx = 0.f, ty = 0.f, tz = 0.f;
   const float fs = (float)spp;
-  for (int i = 0; i < spp; ++i) {
-    const float *s = samples + ((int64_t)i * npix + px) * 3;
-    tx += s[0] / fs;
-    ty += s[1] / fs;
-    tz += s[2] / fs;
+  if ((spp & (spp - 1)) == 0 && spp <= (1 << 24)) {
+    // x / spp == x * (1/spp) for a power of two (both the correctly rounded
+    // x * 2^-k); the loads of 16 samples are issued before their sums (the
+    // kernel is latency-bound: one pixel per thread, spp dependent adds)
+    const float rc = 1.0f / fs;
+    int i = 0;
+    for (; i + 16 <= spp; i += 16) {
+      float v[48];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const float *s = samples + ((int64_t)(i + u) * npix + px) * 3;
+        v[3 * u] = s[0];
+        v[3 * u + 1] = s[1];
+        v[3 * u + 2] = s[2];
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        tx += v[3 * u] * rc;
+        ty += v[3 * u + 1] * rc;
+        tz += v[3 * u + 2] * rc;
+      }
+    }
+    for (; i < spp; ++i) {
+      const float *s = samples + ((int64_t)i * npix + px) * 3;
+      tx += s[0] * rc;
+      ty += s[1] * rc;
+      tz += s[2] * rc;
+    }
+  } else {
+    for (int i = 0; i < spp; ++i) {
+      const float *s = samples + ((int64_t)i * npix + px) * 3;
+      tx += s[0] / fs;
+      ty += s[1] / fs;
+      tz += s[2] / fs;
+    }
   }
   hdr[px * 3] = tx;
   hdr[px * 3 + 1] = ty;
