@@ -1938,7 +1938,11 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
     c = std::min<uint64_t>(std::max<uint64_t>(c, IPT_DYN_MIN_CHUNK), 4096);
     uint64_t units = a.n_samples, small = std::min<uint64_t>(c, IPT_DYN_SMALL_CHUNK);
     if (a.fused) {  // fused pixel mean: chunks of a.chunk pixels (all their samples), small ones of >= 64 samples
+      // a launch with fewer chunks than waves (a thin band) halves them while
+      // that gives the idle waves work and a chunk keeps >= 64 samples: C2's
+      // 1/64 share 0.217 -> 0.10 ms (profiles/r03/launch_scaling_r03w.jsonl)
       c = a.chunk;
+      while (c > 1 && (a.npix + c - 1) / c < waves && (c / 2) * (uint64_t)a.spp >= 64) c /= 2;
       small = std::min<uint64_t>(c, std::max<uint64_t>(1, 64 / (uint64_t)a.spp));
       units = a.npix;
     }
