@@ -11,7 +11,10 @@ vector only"): rank r traces rows r, r + N, ... of the SAME frame
 see `bands_*`; sample seeds are global indices, so the shares are the
 single-GPU frame's samples);
 the forward needs no collective, the adjoint step ends with ONE all-reduce of
-the nT*3 fp64 gradient.  Strong scaling: value = frame samples * K / (max
+the nT*3 fp64 gradient.  Consecutive steps alternate between two HIP streams
+(two frames in flight, each with its own image / gradient buffer), so one
+frame's tail overlaps the next frame's start; `secondary.serial` is the same
+run on one stream.  Strong scaling: value = frame samples * K / (max
 over ranks of the time of K steps).  Inputs are resident in HBM before the
 timed region; timing is HIP events on the launch stream, bracketed by barrier
 + synchronize.
@@ -199,13 +202,19 @@ class Ctx:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    def timed(self, fn, k):
-        """ms for k calls of fn(i) on the stream (barrier-bracketed, max over ranks)."""
+    def timed(self, fn, k, streams=()):
+        """ms for k calls of fn(i) (barrier-bracketed, max over ranks).  With
+        `streams`, fn(i) launches on streams[i % len(streams)]: they start after
+        the region's start event and the region ends when all have drained."""
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         self.barrier()
         e0.record(self.stream)
+        for s in streams:
+            s.wait_event(e0)
         for i in range(k):
             fn(i)
+        for s in streams:
+            self.stream.wait_stream(s)
         e1.record(self.stream)
         self.barrier()
         return self.max_over_ranks(e0.elapsed_time(e1))
@@ -235,30 +244,39 @@ class Leg:
         self.hdr = torch.empty((npix, 3), device=dev, dtype=torch.float32)
         self.adj = torch.full((h, w, 3), 1.0 / (3 * w * h), device=dev, dtype=torch.float32)
         self.grad = torch.zeros((self.sc.nT, 3), device=dev, dtype=torch.float64)
+        # frames in flight (piped=True): consecutive steps alternate between two
+        # streams, each with its own output image and gradient, so one frame's
+        # tail overlaps the next frame's start (the chunk counters are per stream)
+        self.streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+        self.hdr2 = [self.hdr, torch.empty_like(self.hdr)]
+        self.grad2 = [self.grad, torch.zeros_like(self.grad)]
         self.kev = []
 
     def params(self, step):
         return N.make_params(self.w, self.h, self.spp, self.mb, frame_seed(self.seed, step, self.w, self.h, self.spp),
                              self.b, self.e, self.step)
 
-    def fwd(self, step, ev=None):
+    def fwd(self, step, ev=None, piped=False):
         """The HDR image of the rank's rows: ONE launch of the trace kernel with
         the per-pixel mean fused in (brute-force scenes; BVH scenes render
         through the sample buffer + pixel_mean_sm_kernel inside the same call)."""
         cx, p = self.cx, self.params(step)
+        st, hdr = (self.streams[step % 2], self.hdr2[step % 2]) if piped else (cx.stream, self.hdr)
         if ev is not None:
-            ev[0].record(cx.stream)
-        N.check(cx.L.ipt_render_dev(self.sc.handle, C.byref(p), None, self.hdr.data_ptr(), None, cx.st))
+            ev[0].record(st)
+        N.check(cx.L.ipt_render_dev(self.sc.handle, C.byref(p), None, hdr.data_ptr(), None, st.cuda_stream))
         if ev is not None:
-            ev[1].record(cx.stream)
+            ev[1].record(st)
 
-    def adjoint(self, step, reduce=True):
+    def adjoint(self, step, reduce=True, piped=False):
         cx, p = self.cx, self.params(step)
-        self.grad.zero_()
-        N.check(cx.L.ipt_adjoint_dev(self.sc.handle, C.byref(p), None, self.adj.data_ptr(), self.grad.data_ptr(),
-                                     cx.st))
-        if reduce and cx.world > 1:
-            dist.all_reduce(self.grad)  # the per-material gradient vector, nT*3 fp64 (720 B for 30 triangles)
+        st, grad = (self.streams[step % 2], self.grad2[step % 2]) if piped else (cx.stream, self.grad)
+        with torch.cuda.stream(st):
+            grad.zero_()
+            N.check(cx.L.ipt_adjoint_dev(self.sc.handle, C.byref(p), None, self.adj.data_ptr(), grad.data_ptr(),
+                                         st.cuda_stream))
+            if reduce and cx.world > 1:
+                dist.all_reduce(grad)  # the per-material gradient vector, nT*3 fp64 (720 B for 30 triangles)
 
     def samples_per_call(self):
         return self.rows * self.w * self.spp
@@ -278,12 +296,26 @@ def band_table(cx, objs, w, h, spp, mb, n=8, reps=2, interleaved=False):
         leg.adjoint(10**6, reduce=False)
         f = cx.timed(lambda i: leg.fwd(i), reps) / reps
         a = cx.timed(lambda i: leg.adjoint(i, reduce=False), reps) / reps
-        rows.append({"rows": [b, e, st], "fwd_ms": round(f, 4), "adj_ms": round(a, 4)})
+        row = {"rows": [b, e, st], "fwd_ms": round(f, 4), "adj_ms": round(a, 4)}
+        if interleaved:  # per step with two frames in flight (the headline's form)
+            for i in (0, 1):  # both streams' first launches (their chunk counters) outside the timing
+                leg.fwd(i, piped=True)
+                leg.adjoint(i, reduce=False, piped=True)
+            kp = 4 * reps
+            for _ in range(2):  # the first pass settles the streams (allocations, queues); the second counts
+                row["fwd_ms_pipelined"] = round(cx.timed(lambda i: leg.fwd(i, piped=True), kp, leg.streams) / kp, 4)
+                row["adj_ms_pipelined"] = round(cx.timed(lambda i: leg.adjoint(i, reduce=False, piped=True), kp,
+                                                         leg.streams) / kp, 4)
+        rows.append(row)
         leg.close()
     fw = [x["fwd_ms"] for x in rows]
     ad = [x["adj_ms"] for x in rows]
-    return {"bands": rows, "fwd_max_over_mean": round(max(fw) / np.mean(fw), 4),
-            "adj_max_over_mean": round(max(ad) / np.mean(ad), 4)}
+    out = {"bands": rows, "fwd_max_over_mean": round(max(fw) / np.mean(fw), 4),
+           "adj_max_over_mean": round(max(ad) / np.mean(ad), 4)}
+    if interleaved:
+        out["fwd_ms_pipelined_max"] = max(x["fwd_ms_pipelined"] for x in rows)
+        out["adj_ms_pipelined_max"] = max(x["adj_ms_pipelined"] for x in rows)
+    return out
 
 
 def graph_line(cx, seed=0, reps=5):
@@ -348,18 +380,31 @@ def main():
     for i in range(args.warmup):
         head.fwd(10**6 + i)
         head.adjoint(10**6 + i)
+        head.fwd(10**6 + i, piped=True)
+        head.adjoint(10**6 + i, piped=True)
     # ---------------------------------------------------------- headline: tile-split C2 frame
+    # (1) frames one after another on one stream: each launch's own time
+    # (HIP events around it: the roofline's kernel time) and the serial rate
     kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t_wall = time.perf_counter()
-    fwd_ms = cx.timed(lambda i: head.fwd(i, kev[i]), args.steps)
-    wall_fwd = time.perf_counter() - t_wall
+    fwd_serial_ms = cx.timed(lambda i: head.fwd(i, kev[i]), args.steps)
     kernel_ms = float(np.mean([a.elapsed_time(z) for a, z in kev]))
-    bwd_ms = cx.timed(lambda i: head.adjoint(i), args.steps)
+    bwd_serial_ms = cx.timed(lambda i: head.adjoint(i), args.steps)
+    # (2) the headline: consecutive frames alternate between two streams (two
+    # frames in flight: one frame's tail -- its last paths, a few waves per
+    # CU -- overlaps the next frame's start), the same K frames of work
+    t_wall = time.perf_counter()
+    fwd_ms = cx.timed(lambda i: head.fwd(i, piped=True), args.steps, head.streams)
+    wall_fwd = time.perf_counter() - t_wall
+    bwd_ms = cx.timed(lambda i: head.adjoint(i, piped=True), args.steps, head.streams)
     frame = W * H * SPP
     value = args.steps * frame / (fwd_ms / 1e3) / 1e6
     grad_value = args.steps * frame / (bwd_ms / 1e3) / 1e6
 
-    extra = {}
+    extra = {"serial": {"value": round(args.steps * frame / (fwd_serial_ms / 1e3) / 1e6, 2),
+                        "grad_value": round(args.steps * frame / (bwd_serial_ms / 1e3) / 1e6, 2),
+                        "ms_per_step": round(fwd_serial_ms / args.steps, 4),
+                        "grad_ms_per_step": round(bwd_serial_ms / args.steps, 4),
+                        "workload": "the headline's frames one after another on ONE stream (no frame overlap)"}}
     if not args.no_secondary:
         # sustained rates (>= 0.5 s of back-to-back steps per leg; DVFS-steady)
         k, ms = cx.sustained(lambda i: head.fwd(i))
@@ -429,7 +474,7 @@ def main():
     flop_per_launch = band_samples * CASTS_PER_SAMPLE * N_TRIANGLES * FLOP_PER_TEST
     achieved = flop_per_launch / (kernel_ms / 1e3) / 1e12
     # the adjoint kernel over the same casts (its step also holds the gradient memset + all-reduce)
-    grad_achieved = flop_per_launch / (bwd_ms / args.steps / 1e3) / 1e12
+    grad_achieved = flop_per_launch / (bwd_serial_ms / args.steps / 1e3) / 1e12  # the launch's own time
     traffic = None
     if os.path.exists(PMC_FILE):
         with open(PMC_FILE) as f:
@@ -463,7 +508,7 @@ def main():
     if ex:  # the culled casts skip pairs no ray can accept: the work actually issued is smaller
         ea = band_samples * ex / (kernel_ms / 1e3) / 1e12
         roofline["executed_frac"] = round(ea / PEAK_FP32_TFLOPS, 4)
-        roofline["executed_grad_frac"] = round(band_samples * ex / (bwd_ms / args.steps / 1e3) / 1e12 /
+        roofline["executed_grad_frac"] = round(band_samples * ex / (bwd_serial_ms / args.steps / 1e3) / 1e12 /
                                                PEAK_FP32_TFLOPS, 4)
         roofline["executed"] = {"flop_per_sample": round(ex, 1), "achieved": round(ea, 3),
                                 "source": "triangle tests (x38) and slab tests (x12) actually executed, "

@@ -25,6 +25,7 @@
 #   scaling      tools/launch_scaling.py (fixed cost per launch: C2 shares 1/1 .. 1/64)
 #   workflow     tools/workflow_at_size.py (pipeline all --n 100 + optimize --n 100)
 #   graphprof    rocprofv3 --kernel-trace --stats of createGraph at the reference config (tools/graph_prof.py)
+#   pipeab       tools/pipeline_ab.py (consecutive frames on one stream vs two)
 #   envab        tools/env_ab.py $ENVAB (launch-time switches from the environment, A/B)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -82,6 +83,7 @@ run() {
     workflow) timeout -k 10 1000 python -u tools/workflow_at_size.py --out "$OUT/workflow_$T.json" > "$OUT/workflow_$T.log" 2>&1 ;;
     graphprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/graphprof_$T" -o run --output-format csv \
                    -- python3 "$R/tools/graph_prof.py" --steps 20 > "$OUT/graphprof_$T.log" 2>&1 ;;
+    pipeab) timeout -k 10 300 python tools/pipeline_ab.py > "$OUT/pipeab_$T.log" 2>&1 ;;
     envab) timeout -k 10 400 python tools/env_ab.py ${ENVAB:-base:} > "$OUT/envab_$T.log" 2>&1 ;;
     *) echo "unknown stage $1" >&2; return 2 ;;
   esac
