@@ -395,7 +395,10 @@ def main():
     t_wall = time.perf_counter()
     fwd_ms = cx.timed(lambda i: head.fwd(i, piped=True), args.steps, head.streams)
     wall_fwd = time.perf_counter() - t_wall
-    bwd_ms = cx.timed(lambda i: head.adjoint(i, piped=True), args.steps, head.streams)
+    # (gloo, the one-GPU rehearsal backend, stages every all-reduce through the
+    # host: there the adjoint steps stay on one stream)
+    piped_adj = world == 1 or backend == "nccl"
+    bwd_ms = cx.timed(lambda i: head.adjoint(i, piped=piped_adj), args.steps, head.streams if piped_adj else ())
     frame = W * H * SPP
     value = args.steps * frame / (fwd_ms / 1e3) / 1e6
     grad_value = args.steps * frame / (bwd_ms / 1e3) / 1e6
