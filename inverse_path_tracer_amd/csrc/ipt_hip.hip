@@ -82,6 +82,10 @@ constexpr int kBlock = 256;
 constexpr int kRecSD = 3;  // specd, then speci
 constexpr int kRecFieldsDiffuse = 3;
 constexpr int kRecFieldsSpec = kRecFieldsDiffuse + 2;
+// ADJU (records in global memory): the three words of the prefix throughput
+// M_k follow, so the sweep reads M_kk instead of refolding it from the
+// chunk's first record (O(K) per path, not O(K^2))
+#define kRecMU (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse)
 constexpr int kMaxAdjTris = 65535;  // tri and et share one 32-bit field
 constexpr int kEdgeW = 8;      // graph bin: w, w*f, pix[3]*w*f, light[3]*w*f
 // LDS form of the graph bins: 5 doubles per (dst, src) (w, w*f, pix[3]*w*f)
@@ -93,13 +97,15 @@ __host__ __device__ inline size_t graph_lds_doubles(int nT, int nE) {
   return (size_t)(nT + 1) * nT * kEdgeL + (size_t)(nT + 1) * (nE > 0 ? nE : 0) * 3;
 }
 constexpr int kMaxAdjBounces = 62;
-// ADJU ring slots per lane: 8 x 3 words x 256 lanes = 24 KB of LDS (6
-// workgroups per CU).  Paths of more than 8 vertices replay their earlier
-// chunks (Russian roulette keeps 90% per bounce and the box is open at the
-// front, so long paths are a small minority; a path of K vertices costs
-// about K^2 / 16 extra vertex traces).
+// ADJU ring slots per lane, in global memory (TraceArgs::grec: 3 words x 64
+// slots x the grid's lanes, 251 MB at C3, stream-ordered scratch; the
+// records of the live vertices stay in L2 / MALL).  Paths of more than 64
+// vertices replay their earlier chunks (a path of K vertices costs about
+// K^2 / 128 extra vertex traces).  Round 2 kept an 8-slot ring in LDS (24 KB
+// per workgroup): every path longer than 8 vertices replayed, C3 unbounded
+// adjoint 5.97 ms for a 2.73 ms forward.
 #ifndef IPT_ADJU_RING
-#define IPT_ADJU_RING 8
+#define IPT_ADJU_RING 64
 #endif
 constexpr int kAdjuRing = IPT_ADJU_RING;
 // Dynamic work distribution across the waves of a launch (TraceArgs::chunk):
@@ -186,6 +192,8 @@ struct TraceArgs {
   float rc_spp;
   float rc_W, rc_H;  // 1/W, 1/H for power-of-two sizes, else 0 (camera_ray divides)
   int rec_cap;   // ADJ: vertex records per lane (max_bounces + 1); ADJU: ring slots
+  float *grec;   // ADJU: the record ring in global memory, 3 fields x rec_cap slots x grec_stride lanes
+  uint64_t grec_stride;
   // scene batch (C5): blocks b, b + nscenes, ... (bps of them) trace material
   // set b -- interleaved, not contiguous ranges: the dispatcher fills a CU
   // with consecutive workgroups, so contiguous ranges gave some sets fewer
@@ -583,7 +591,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   float *lds_rec = a.small_pairs ? reinterpret_cast<float *>(lds_po) + (po ? nT * nE : 0) : lds_e3;
   // MODE_ADJ: one word per lane (the sweep's owner markers) in front of the
   // vertex records
-  if (MODE == MODE_ADJ) lds_rec += kBlock;
+  if (is_adj<MODE>()) lds_rec += kBlock;
   BvhView bv;
   bv.isect = isect;
   bv.big = nullptr;
@@ -601,7 +609,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   cv.stride = a.coop_stride;
   for (int k = 0; k < 6; ++k) cv.root[k] = a.root_box[k];
   if (BVH) {
-    const size_t rec_words = is_adj<MODE>() ? (size_t)vmax * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock : 0;
+    const size_t rec_words = MODE == MODE_ADJ ? (size_t)vmax * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock : 0;  // (ADJU: global)
     char *base = reinterpret_cast<char *>(lds);
     const size_t off = bvh_lds_offset((size_t)(reinterpret_cast<char *>(lds_rec + rec_words) - base));
     float4 *lw = reinterpret_cast<float4 *>(base + off);
@@ -647,6 +655,14 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     }
   };
 
+  // MODE_ADJU: the vertex-record ring lives in global memory (TraceArgs::grec,
+  // [field][slot][lane of the grid]: a lane's records are ustride floats apart)
+  gbl_f32 *urec = nullptr;
+  size_t ustride = 0;
+  if (MODE == MODE_ADJU) {
+    ustride = a.grec_stride;
+    urec = (gbl_f32 *)a.grec + (size_t)blockIdx.x * kBlock + tid;
+  }
   {  // the wave's persistent loop
   // wave-uniform sample range (static partition, regenerated per lane)
   const uint32_t wave = __builtin_amdgcn_readfirstlane((sblock * kBlock + tid) >> 6);
@@ -681,9 +697,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   Rng st;
   V3 p = mk(0.f, 0.f, 0.f), d = p;
   V3 L = p, Le = p, Ld = p, M = mk(1.f, 1.f, 1.f);
-  // ADJU (unbounded adjoint): throughput at the oldest ring record, suffix
-  // carried from the chunk after, replay target (0 = first pass), next slot
-  V3 Mlo = M, Scar = mk(0.f, 0.f, 0.f);
+  // ADJU (unbounded adjoint): suffix carried from the chunk after, replay
+  // target (0 = first pass), next ring slot
+  V3 Scar = mk(0.f, 0.f, 0.f);
   int rhi = 0, rslot = 0;
   float weight = 1.f;  // GRAPH path weight
   V3 pix = p;          // GRAPH target pixel
@@ -807,7 +823,6 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           M = mk(1.f, 1.f, 1.f);
           k = 0;
           if (MODE == MODE_ADJU) {
-            Mlo = M;
             rhi = 0;
             rslot = 0;
           }
@@ -1033,20 +1048,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           rec[(kRecSD + 1) * fs] = speci;
         }
       }
-      if (MODE == MODE_ADJU) {  // ring slot rslot = k % rec_cap; evicting vertex k - rec_cap folds it into Mlo
-        float *rec = lds_rec + (size_t)rslot * kBlock + tid;
-        const size_t fs = (size_t)vmax * kBlock;
-        if (k >= vmax) {  // Mlo <- M_{k - rec_cap + 1}, with the forward's own operations
-          const int tj = (int)(__float_as_uint(rec[0]) & 0xffffu);
-          const float cj = rec[2 * fs];
-          V3 tv = kdpi3(tj);
-          if (SPEC) {
-            const TriMat &mj = mat[tj];
-            const float si = rec[(kRecSD + 1) * fs];
-            tv = mk(tv.x + mj.ks[0] * si, tv.y + mj.ks[1] * si, tv.z + mj.ks[2] * si);
-          }
-          Mlo = mk((Mlo.x * tv.x) * cj, (Mlo.y * tv.y) * cj, (Mlo.z * tv.z) * cj);
-        }
+      if (MODE == MODE_ADJU) {  // ring slot rslot = k % rec_cap (global memory), with the prefix throughput M_k
+        gbl_f32 *rec = urec + (size_t)rslot * ustride;
+        const size_t fs = (size_t)vmax * ustride;
         rec[0] = __uint_as_float((uint32_t)tri | ((uint32_t)emit_et << 16));
         rec[fs] = emit_s;
         rec[2 * fs] = coeff;
@@ -1054,6 +1058,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           rec[kRecSD * fs] = specd;
           rec[(kRecSD + 1) * fs] = speci;
         }
+        rec[kRecMU * fs] = M.x;  // M before this vertex's update: the forward's own M_k
+        rec[(kRecMU + 1) * fs] = M.y;
+        rec[(kRecMU + 2) * fs] = M.z;
         rslot = (rslot + 1 == vmax) ? 0 : rslot + 1;
       }
       if (MODE == MODE_GRAPH) {
@@ -1082,6 +1089,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       if (MODE == MODE_ADJU && rhi > 0 && k == rhi) finished = true;  // replay reached its chunk's end
     }
 
+    int uhi = 0, ulo = 0;  // ADJU: the chunk [ulo, uhi) to sweep, ufirst = the path's first pass
+    bool ufirst = false;
     if (finished) {
       active = false;
       if (MODE == MODE_FWDM) {
@@ -1097,101 +1106,13 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         o[1] = L.y;
         o[2] = L.z;
       } else if (MODE == MODE_ADJU) {
-        // Sweep the chunk [lo, hi) held by the ring: hi = K (first pass; the
-        // escape terms of the path's end apply) or the replay target.  Same
-        // operations as the per-lane sweep below / the oracle's
-        // adjoint_sample: prefix throughputs folded from Mlo = M_lo, the
-        // suffix S from the chunk after (Scar) or the escape term.
-        const bool first = rhi == 0;
-        const int hi = first ? k : rhi;
-        const int lo = hi > vmax ? hi - vmax : 0;
-        if (hi > 0) {
-          const size_t fs = (size_t)vmax * kBlock;
-          const uint64_t pixel = item_pixel(a, witem);
-          const float ax = adj[pixel * 3 + 0] / (float)a.spp;
-          const float ay = adj[pixel * 3 + 1] / (float)a.spp;
-          const float az = adj[pixel * 3 + 2] / (float)a.spp;
-          auto col = [&](int v) {  // record of vertex v in [lo, hi): ring slot v % rec_cap
-            int sl = rslot - (hi - v);
-            sl = sl < 0 ? sl + vmax : sl;
-            return lds_rec + (size_t)sl * kBlock + tid;
-          };
-          auto rec_lo = [&](const float *r) {  // the forward's lo, same products
-            const V3 kee = ke3((int)(__float_as_uint(r[0]) >> 16));
-            return mk(kee.x * r[fs], kee.y * r[fs], kee.z * r[fs]);
-          };
-          auto tdiff = [&](const float *r) {  // T_j = kd/pi (+ Ks*speci)
-            const int tj = (int)(__float_as_uint(r[0]) & 0xffffu);
-            V3 x = kdpi3(tj);
-            if (SPEC) {
-              const TriMat &mj = mat[tj];
-              const float si = r[(kRecSD + 1) * fs];
-              x = mk(x.x + mj.ks[0] * si, x.y + mj.ks[1] * si, x.z + mj.ks[2] * si);
-            }
-            return x;
-          };
-          auto ddir = [&](const float *r) {  // D_j = kd (+ Ks*specd)
-            const int tj = (int)(__float_as_uint(r[0]) & 0xffffu);
-            V3 x = kd3(tj);
-            if (SPEC) {
-              const TriMat &mj = mat[tj];
-              const float sd = r[kRecSD * fs];
-              x = mk(x.x + mj.ks[0] * sd, x.y + mj.ks[1] * sd, x.z + mj.ks[2] * sd);
-            }
-            return x;
-          };
-          V3 S = Scar;
-          if (first) {
-            S = mk(0.f, 0.f, 0.f);
-            if (escaped) {
-              const float *r = col(hi - 1);
-              const V3 lk = rec_lo(r), dj = ddir(r);
-              S = mk(Le.x + dj.x * lk.x, Le.y + dj.y * lk.y, Le.z + dj.z * lk.z);
-            }
-          }
-          for (int kk = hi - 1; kk >= lo; --kk) {
-            V3 Mk = Mlo;
-            for (int j = lo; j < kk; ++j) {
-              const float *rj = col(j);
-              const float cj = rj[2 * fs];
-              const V3 tv = tdiff(rj);
-              Mk = mk((Mk.x * tv.x) * cj, (Mk.y * tv.y) * cj, (Mk.z * tv.z) * cj);
-            }
-            const float *r = col(kk);
-            const int tk = (int)(__float_as_uint(r[0]) & 0xffffu);
-            const V3 lk = rec_lo(r);
-            const float ck = r[2 * fs];
-            const bool last_esc = first && escaped && kk == hi - 1;
-            const bool continued = !first || kk < hi - 1 || escaped;
-            V3 dLd = Mk;
-            if (last_esc) dLd = mk(dLd.x + M.x, dLd.y + M.y, dLd.z + M.z);
-            V3 gk = mk(dLd.x * lk.x, dLd.y * lk.y, dLd.z * lk.z);
-            if (continued) {
-              const float cpi = ck / kPiF;
-              gk = mk(gk.x + (cpi * Mk.x) * S.x, gk.y + (cpi * Mk.y) * S.y, gk.z + (cpi * Mk.z) * S.z);
-            }
-            const int sl = a.grad_map ? a.grad_map[tk] : tk;
-            const double v[3] = {(double)(ax * gk.x), (double)(ay * gk.y), (double)(az * gk.z)};
-            bins_add(sl >= 0, grad, sl >= 0 ? (size_t)sl * 3 : (size_t)tk * 3, 3, v);
-            const V3 dj = ddir(r), tv = tdiff(r);
-            S = mk((Le.x + dj.x * lk.x) + (tv.x * ck) * S.x, (Le.y + dj.y * lk.y) + (tv.y * ck) * S.y,
-                   (Le.z + dj.z * lk.z) + (tv.z * ck) * S.z);
-          }
-          Scar = S;  // S_lo: the suffix the previous chunk's last vertex continues into
-        }
-        if (lo > 0) {  // replay the path from its camera ray to re-record [lo - rec_cap, lo)
-          int r, c;
-          item_ray(a, seed, witem, st, p, d, r, c);
-          L = mk(0.f, 0.f, 0.f);
-          Le = L;
-          Ld = L;
-          M = mk(1.f, 1.f, 1.f);
-          Mlo = M;
-          k = 0;
-          rslot = 0;
-          rhi = lo;
-          active = true;
-        }
+        // the chunk [lo, hi) held by the ring -- hi = K (first pass; the
+        // escape terms of the path's end apply) or the replay target -- is
+        // swept by the wave-parallel sweep below; then, if lo > 0, the path
+        // is replayed from its camera ray to re-record [lo - rec_cap, lo)
+        ufirst = rhi == 0;
+        uhi = ufirst ? k : rhi;
+        ulo = uhi > vmax ? uhi - vmax : 0;
       }
     }
     if (MODE == MODE_FWDM) {
@@ -1242,7 +1163,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         }
       }
     }
-    if (MODE == MODE_ADJ) {
+    if (is_adj<MODE>()) {
       // Wave-parallel backward sweep (oracle adjoint_sample).  The vertices of
       // the paths that finished in this iteration become tasks (path, vertex
       // kk), packed into rounds of <= 64 consecutive lanes without splitting a
@@ -1254,7 +1175,12 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       // sweep (only the order of the fp64 gradient atomics changes).  Round 2
       // recomputed both chains per task from the owner's LDS column (O(K^2)
       // record reads, loops as long as the wave's longest chain).
-      const int Kf = (finished && k > 0) ? k : 0;
+      // MODE_ADJU sweeps the chunk [ulo, uhi) of each finished lane the same
+      // way, from its records in global memory: there the prefix throughputs
+      // are recorded (no left-to-right chain), the last task's suffix is the
+      // chunk after's (Scar) unless this is the path's first pass, and the
+      // suffix at ulo goes back to the owner for its replay.
+      const int Kf = MODE == MODE_ADJ ? ((finished && k > 0) ? k : 0) : ((finished && uhi > 0) ? uhi - ulo : 0);
 #ifdef IPT_ABL_NOWSWEEP  // timing-only ablation build: no backward sweep (no gradients)
       if (0) {
 #else
@@ -1278,7 +1204,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             wz = adj[pixel * 3 + 2] / (float)a.spp;
           }
         }
-        const size_t fs = (size_t)vmax * kBlock;
+        const size_t fs = MODE == MODE_ADJ ? (size_t)vmax * kBlock : (size_t)vmax * ustride;
         int base = 0;
         while (base < T) {  // wave-uniform
           // this round: the whole paths whose tasks end by base + 64
@@ -1287,31 +1213,57 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           const int t = base + lane;
           const bool valid = t < next;
           // owners of this round mark their first task's lane with (start,
-          // escaped, K, owner lane) + 1 -- start in the top bits, so an
-          // inclusive max-scan leaves every task lane the marker of the last
-          // owner starting at or before it: its own path
+          // first pass, escaped, K, owner lane) + 1 -- start in the top bits,
+          // so an inclusive max-scan leaves every task lane the marker of the
+          // last owner starting at or before it: its own path
           swl[lane] = 0u;
           const int st0 = inc - Kf - base;
-          if (Kf > 0 && inc <= next && st0 >= 0)
-            swl[st0] = (((uint32_t)st0 << 13) | (escaped ? 1u << 12 : 0u) | ((uint32_t)Kf << 6) | (uint32_t)lane) + 1u;
+          const bool owns = Kf > 0 && inc <= next && st0 >= 0;
+          if (owns)
+            swl[st0] = (((uint32_t)st0 << 15) | (ufirst ? 1u << 14 : 0u) | (escaped ? 1u << 13 : 0u) |
+                        ((uint32_t)Kf << 6) | (uint32_t)lane) + 1u;
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
           const uint32_t mk_ = wave_scan_max(swl[lane]) - 1u;
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // read before the next round's marks
           __builtin_amdgcn_wave_barrier();
           const int ow = valid ? (int)(mk_ & 63u) : lane;
-          const int KL = valid ? (int)((mk_ >> 6) & 63u) : 0;
-          const int kk = valid ? lane - (int)(mk_ >> 13) : 0;
-          const bool esc_o = valid && ((mk_ >> 12) & 1u);
+          const int KL = valid ? (int)((mk_ >> 6) & 127u) : 0;
+          const int kk = valid ? lane - (int)(mk_ >> 15) : 0;  // task index inside the path's chunk
+          const bool esc = valid && ((mk_ >> 13) & 1u);
+          const bool fst_o = MODE == MODE_ADJ || (valid && ((mk_ >> 14) & 1u));
           const int rr = valid ? KL - 1 - kk : 0;  // vertices after this one
-          const bool esc = esc_o;
           const float ax = __shfl(wx, ow), ay = __shfl(wy, ow), az = __shfl(wz, ow);
           const V3 LeL = mk(__shfl(Le.x, ow), __shfl(Le.y, ow), __shfl(Le.z, ow));
           const V3 ML = mk(__shfl(M.x, ow), __shfl(M.y, ow), __shfl(M.z, ow));
           // this task's record (lanes past the round read vertex 0 of a valid column)
-          const float *r = lds_rec + (tid & ~63) + (valid ? ow : lane) + (size_t)kk * kBlock;
-          const uint32_t f0 = valid ? __float_as_uint(r[0]) : 0u;
-          const float es = r[fs], ck = r[2 * fs];
+          uint32_t f0;
+          float es, ck, sdv = 0.f, si = 0.f;
+          V3 Mk = mk(1.f, 1.f, 1.f);
+          V3 Sc = mk(0.f, 0.f, 0.f);  // ADJU: the owner's suffix from the chunk after
+          if (MODE == MODE_ADJ) {
+            const float *r = lds_rec + (tid & ~63) + (valid ? ow : lane) + (size_t)kk * kBlock;
+            f0 = valid ? __float_as_uint(r[0]) : 0u;
+            es = r[fs];
+            ck = r[2 * fs];
+            if (SPEC) {
+              sdv = r[kRecSD * fs];
+              si = r[(kRecSD + 1) * fs];
+            }
+          } else {
+            const int vabs = kk + __shfl(ulo, ow);  // the vertex's index on its path: ring slot vabs % rec_cap
+            const gbl_f32 *r = (const gbl_f32 *)a.grec + (size_t)blockIdx.x * kBlock + (tid & ~63) +
+                               (valid ? ow : lane) + (size_t)(vabs % vmax) * ustride;
+            f0 = valid ? __float_as_uint(r[0]) : 0u;
+            es = r[fs];
+            ck = r[2 * fs];
+            if (SPEC) {
+              sdv = r[kRecSD * fs];
+              si = r[(kRecSD + 1) * fs];
+            }
+            Mk = mk(r[kRecMU * fs], r[(kRecMU + 1) * fs], r[(kRecMU + 2) * fs]);  // the forward's own M_kk
+            Sc = mk(__shfl(Scar.x, ow), __shfl(Scar.y, ow), __shfl(Scar.z, ow));
+          }
           // (the min()s keep a mis-indexed record from reaching global memory out of bounds)
           const int tk = min((int)(f0 & 0xffffu), nT - 1);
           const V3 kee = ke3(min((int)(f0 >> 16), nT - 1));
@@ -1319,32 +1271,33 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           V3 dj = kd3(tk), tv = kdpi3(tk);  // D = kd (+ Ks*specd), T = kd/pi (+ Ks*speci)
           if (SPEC) {
             const TriMat &mj = mat[tk];
-            const float sdv = r[kRecSD * fs], si = r[(kRecSD + 1) * fs];
             dj = mk(dj.x + mj.ks[0] * sdv, dj.y + mj.ks[1] * sdv, dj.z + mj.ks[2] * sdv);
             tv = mk(tv.x + mj.ks[0] * si, tv.y + mj.ks[1] * si, tv.z + mj.ks[2] * si);
           }
-          // prefix: M_0 = 1, M_s = (M_{s-1} * T_{s-1}) * c_{s-1} from the left neighbour
-          V3 Mk = mk(1.f, 1.f, 1.f);
-          // suffix: S_K = escaped ? Le + D_{K-1} lo_{K-1} : 0, S_j = (Le + D_j lo_j) + (T_j c_j) S_{j+1}
+          // prefix (ADJ): M_0 = 1, M_s = (M_{s-1} * T_{s-1}) * c_{s-1} from the left neighbour
+          // suffix: S_K = escaped ? Le + D_{K-1} lo_{K-1} : 0 (ADJU replay chunks: Scar),
+          // S_j = (Le + D_j lo_j) + (T_j c_j) S_{j+1}
           const V3 A = mk(LeL.x + dj.x * lk.x, LeL.y + dj.y * lk.y, LeL.z + dj.z * lk.z);
           const V3 B = mk(tv.x * ck, tv.y * ck, tv.z * ck);
           V3 S = (esc && rr == 0) ? A : mk(0.f, 0.f, 0.f);
+          if (MODE == MODE_ADJU && !fst_o && rr == 0) S = Sc;
+          const int kkp = MODE == MODE_ADJ ? kk : 0;  // ADJU: no prefix chain
           // both chains in one loop (max(K) - 1 steps instead of up to twice
           // that; two independent dependency chains per step: -0.2..0.6%,
           // profiles/r03/variants_merged_r03o.log)
-          for (int s = 1; __ballot(valid && (kk >= s || rr >= s)); ++s) {
+          for (int s = 1; __ballot(valid && (kkp >= s || rr >= s)); ++s) {
             const V3 N = mk((Mk.x * tv.x) * ck, (Mk.y * tv.y) * ck, (Mk.z * tv.z) * ck);
             const V3 H = mk(A.x + B.x * S.x, A.y + B.y * S.y, A.z + B.z * S.z);
             const V3 Nl = mk(wave_shr1(N.x), wave_shr1(N.y), wave_shr1(N.z));
             const V3 Hr = mk(wave_shl1(H.x), wave_shl1(H.y), wave_shl1(H.z));
-            if (kk == s) Mk = Nl;
+            if (kkp == s) Mk = Nl;
             if (rr == s) S = Hr;
           }
           if (valid) {
             V3 dLd = Mk;
             if (esc && rr == 0) dLd = mk(dLd.x + ML.x, dLd.y + ML.y, dLd.z + ML.z);
             V3 gk = mk(dLd.x * lk.x, dLd.y * lk.y, dLd.z * lk.z);
-            if (rr > 0 || esc) {
+            if (rr > 0 || esc || !fst_o) {
               const float cpi = ck / kPiF;
               gk = mk(gk.x + (cpi * Mk.x) * S.x, gk.y + (cpi * Mk.y) * S.y, gk.z + (cpi * Mk.z) * S.z);
             }
@@ -1356,8 +1309,26 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             bins_add(sl >= 0, grad, sl >= 0 ? (size_t)sl * 3 : (size_t)tk * 3, 3, v);
 #endif
           }
+          if (MODE == MODE_ADJU) {  // the suffix at the chunk's first vertex, S_lo = A + B S, back to its owner
+            const V3 H = mk(A.x + B.x * S.x, A.y + B.y * S.y, A.z + B.z * S.z);
+            const int sa = (owns ? st0 : lane) << 2;
+            const V3 Hs = mk(bperm_f(sa, H.x), bperm_f(sa, H.y), bperm_f(sa, H.z));
+            if (owns) Scar = Hs;
+          }
           base = next;
         }
+      }
+      if (MODE == MODE_ADJU && finished && ulo > 0) {  // replay the path to re-record [ulo - rec_cap, ulo)
+        int r, c;
+        item_ray(a, seed, witem, st, p, d, r, c);
+        L = mk(0.f, 0.f, 0.f);
+        Le = L;
+        Ld = L;
+        M = mk(1.f, 1.f, 1.f);
+        k = 0;
+        rslot = 0;
+        rhi = ulo;
+        active = true;
       }
     }
     PHASE(5)
@@ -1772,6 +1743,8 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
     a.cam_org[i] = std::fmaf(M[3], 1.f, std::fmaf(M[2], 0.f, std::fmaf(M[1], 0.f, M[0] * 0.f)));
   }
   a.rec_cap = p.max_bounces >= 0 ? p.max_bounces + 1 : 0;
+  a.grec = nullptr;
+  a.grec_stride = 0;
   a.chunk = 0;
   a.chunk_small = 0;
   a.chunk_big_n = 0;
@@ -1957,6 +1930,13 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
     cap_ctr.st = st;
     if (stream_counters(s, st, a.nscenes, (uint32_t)grabs, &b.chunk_ctr, &b.chunk_base, &cap_ctr.p, &ctr_lock))
       return -1;
+  }
+  StreamScratch grec;  // ADJU: the vertex-record ring (TraceArgs::grec), freed behind the launch
+  if (MODE == MODE_ADJU) {
+    b.grec_stride = (uint64_t)grid * kBlock;
+    const size_t fields = (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) + 3;  // + M_k (kRecMU)
+    if (grec.alloc(fields * (size_t)a.rec_cap * b.grec_stride * sizeof(float), st)) return -1;
+    b.grec = (float *)grec.p;
   }
   hipLaunchKernelGGL((trace_kernel<MODE, SPEC, BVH>), dim3(grid), dim3(kBlock), lds, st, b, s->isect, s->pairs, s->geom,
                      s->mat, kd_dev ? kd_dev : s->kd, s->emit_tri, s->emit_cdf, s->emit_pmf, out, adj, grad, target,
@@ -2161,8 +2141,10 @@ int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const f
   }
   if (unbounded) a.rec_cap = kAdjuRing;
   const size_t lds = (size_t)a.grad_slots * 3 * sizeof(double) + table_bytes(a) +
-                     (!unbounded ? (size_t)kBlock * sizeof(uint32_t) : 0) +
-                     (size_t)a.rec_cap * (s->has_ks ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock * sizeof(float);
+                     (size_t)kBlock * sizeof(uint32_t) +  // the sweep's owner markers
+                     (!unbounded ? (size_t)a.rec_cap * (s->has_ks ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock *
+                                       sizeof(float)
+                                 : 0);  // (ADJU: the record ring is in global memory, launch_inst)
   if (lds > 160 * 1024) {
     gpu_set_error("adjoint LDS footprint exceeds 160 KiB; lower max_bounces");
     return -1;

@@ -97,7 +97,8 @@ def main():
         pb = N.make_params(512, 512, 64, 4, 0, 192, 256)  # one 64-row band: a small launch (the 8-GPU share)
         pr8 = N.make_params(512, 512, 64, 4, 0, 0, 512, 8)  # one interleaved 1/8 share (the bench's tile split)
         hdr = torch.empty((512 * 512, 3), device=dev)
-        kinds = ("fwd", "fsm", "adj", "band", "render", "render8", "adj8")
+        pu = N.make_params(512, 512, 64, None, 0)  # the reference's own estimator (no bounce cap)
+        kinds = ("fwd", "fsm", "adj", "band", "render", "render8", "adj8", "adju")
         times = {n: {k: [] for k in kinds} for n in libs}
         for rnd in range(6):
             for n, L in libs.items():
@@ -116,6 +117,8 @@ def main():
                         elif kind in ("render", "render8"):
                             pp = p if kind == "render" else pr8
                             assert L.ipt_render_dev(hs[n], C.byref(pp), None, hdr.data_ptr(), None, st) == 0
+                        elif kind == "adju":
+                            assert L.ipt_adjoint_dev(hs[n], C.byref(pu), None, adj.data_ptr(), g.data_ptr(), st) == 0
                         elif kind == "adj8":
                             assert L.ipt_adjoint_dev(hs[n], C.byref(pr8), None, adj.data_ptr(), g.data_ptr(), st) == 0
                         else:
@@ -132,6 +135,7 @@ def main():
                                     "render_ms": round(float(np.median(times[n]["render"])), 4),
                                     "render8_ms": round(float(np.median(times[n]["render8"])), 4),
                                     "adj8_ms": round(float(np.median(times[n]["adj8"])), 4),
+                                    "adju_ms": round(float(np.median(times[n]["adju"])), 4),
                                     "fwd_Msps": round(512 * 512 * 64 / f / 1e3, 1), "adj_Msps": round(512 * 512 * 64 / a / 1e3, 1)}
             print(sname, n, out[sname + ":" + n], flush=True)
     print(json.dumps(out))
