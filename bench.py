@@ -247,6 +247,9 @@ class Leg:
         # frames in flight (piped=True): consecutive steps alternate between two
         # streams, each with its own output image and gradient, so one frame's
         # tail overlaps the next frame's start (the chunk counters are per stream)
+        # (the headline's Leg is the process's first: HIP maps streams onto a
+        # few hardware queues in creation order, and two streams sharing one
+        # run in order; measured per-share overlap: tools/pipeline_ab.py)
         self.streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
         self.hdr2 = [self.hdr, torch.empty_like(self.hdr)]
         self.grad2 = [self.grad, torch.zeros_like(self.grad)]
@@ -296,26 +299,12 @@ def band_table(cx, objs, w, h, spp, mb, n=8, reps=2, interleaved=False):
         leg.adjoint(10**6, reduce=False)
         f = cx.timed(lambda i: leg.fwd(i), reps) / reps
         a = cx.timed(lambda i: leg.adjoint(i, reduce=False), reps) / reps
-        row = {"rows": [b, e, st], "fwd_ms": round(f, 4), "adj_ms": round(a, 4)}
-        if interleaved:  # per step with two frames in flight (the headline's form)
-            for i in (0, 1):  # both streams' first launches (their chunk counters) outside the timing
-                leg.fwd(i, piped=True)
-                leg.adjoint(i, reduce=False, piped=True)
-            kp = 4 * reps
-            for _ in range(2):  # the first pass settles the streams (allocations, queues); the second counts
-                row["fwd_ms_pipelined"] = round(cx.timed(lambda i: leg.fwd(i, piped=True), kp, leg.streams) / kp, 4)
-                row["adj_ms_pipelined"] = round(cx.timed(lambda i: leg.adjoint(i, reduce=False, piped=True), kp,
-                                                         leg.streams) / kp, 4)
-        rows.append(row)
+        rows.append({"rows": [b, e, st], "fwd_ms": round(f, 4), "adj_ms": round(a, 4)})
         leg.close()
     fw = [x["fwd_ms"] for x in rows]
     ad = [x["adj_ms"] for x in rows]
-    out = {"bands": rows, "fwd_max_over_mean": round(max(fw) / np.mean(fw), 4),
-           "adj_max_over_mean": round(max(ad) / np.mean(ad), 4)}
-    if interleaved:
-        out["fwd_ms_pipelined_max"] = max(x["fwd_ms_pipelined"] for x in rows)
-        out["adj_ms_pipelined_max"] = max(x["adj_ms_pipelined"] for x in rows)
-    return out
+    return {"bands": rows, "fwd_max_over_mean": round(max(fw) / np.mean(fw), 4),
+            "adj_max_over_mean": round(max(ad) / np.mean(ad), 4)}
 
 
 def graph_line(cx, seed=0, reps=5):
