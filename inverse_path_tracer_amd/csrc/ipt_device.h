@@ -44,6 +44,27 @@ constexpr float kPiF = 3.14159265358979323846f;        // (float)M_PI
 constexpr float kInvPiF = (float)(1.0 / 3.14159265358979323846);  // (float)(1/M_PI)
 constexpr double kPi = 3.14159265358979323846;
 
+// x / b for the constant divisors b = kInvPiF, kPRR, kPiF in three VALU
+// operations (Markstein: q = x*y, r = fma(-q, b, x) exact, fma(r, y, q)),
+// with y = RN(1/b).  Equal to the IEEE quotient for every float 2^-100 <= |x|
+// < 2^100 -- checked exhaustively for these three b (tools/check_div_const.c,
+// tests/test_identities.py); other x (zeros, tiny, huge, non-finite) take
+// the IEEE division.  Not a generic division: only those three divisors.
+#ifndef IPT_DIV_CONST
+#define IPT_DIV_CONST 1
+#endif
+template <int B>  // 0: kInvPiF, 1: kPRR, 2: kPiF
+__device__ __forceinline__ float div_const(float x) {
+  constexpr float b = B == 0 ? kInvPiF : (B == 1 ? kPRR : kPiF);
+  constexpr float y = (float)(1.0 / (double)b);
+  const float ax = fabsf(x);
+  if (IPT_DIV_CONST && ax >= 0x1p-100f && ax < 0x1p100f) {
+    const float q = x * y;
+    return fmaf(fmaf(-q, b, x), y, q);
+  }
+  return x / b;
+}
+
 // ------------------------------------------------------------ XORWOW
 struct Rng {
   uint32_t d, v0, v1, v2, v3, v4;

@@ -948,7 +948,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
                        fmaf(g.R[2][2], h.z, fmaf(g.R[2][1], h.y, g.R[2][0] * h.x))));
           if (MODE != MODE_GRAPH) {
             if (SPEC && (m.flags & MAT_HAS_KS)) speci = phong(m.shininess, nh, din, nd);
-            coeff = (dot3(nd, nh) / psamp) / kPRR;
+            coeff = spec ? (dot3(nd, nh) / psamp) / kPRR : div_const<1>(div_const<0>(dot3(nd, nh)));  // psamp = kInvPiF
           }
           cont = true;
         }
@@ -1298,7 +1298,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             if (esc && rr == 0) dLd = mk(dLd.x + ML.x, dLd.y + ML.y, dLd.z + ML.z);
             V3 gk = mk(dLd.x * lk.x, dLd.y * lk.y, dLd.z * lk.z);
             if (rr > 0 || esc || !fst_o) {
-              const float cpi = ck / kPiF;
+              const float cpi = div_const<2>(ck);  // ck / kPiF
               gk = mk(gk.x + (cpi * Mk.x) * S.x, gk.y + (cpi * Mk.y) * S.y, gk.z + (cpi * Mk.z) * S.z);
             }
             const int sl = a.grad_map ? a.grad_map[tk] : tk;

@@ -71,3 +71,22 @@ def test_lemire_division_exact():
         for n in ns + [d - 1, d, d + 1, 2 * d - 1, (2**32 - 1) // d * d, (2**32 - 1) // d * d - 1]:
             if 0 <= n < 2**32:
                 assert (m * n) >> 64 == n // d, (n, d)
+
+
+def test_div_const_equals_ieee_exhaustive(tmp_path):
+    """ipt_device.h::div_const (x / b for b = 1/pi, 0.9, pi in three VALU
+    operations) equals the IEEE quotient for every float 2^-100 <= x < 2^100:
+    tools/check_div_const.c, compiled here (gcc -mfma -fopenmp), ~3 s."""
+    import os
+    import shutil
+    import subprocess
+
+    gcc = shutil.which("gcc")
+    assert gcc, "gcc is needed for the exhaustive check"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "check_div_const")
+    subprocess.run([gcc, "-O2", "-mfma", "-fopenmp", os.path.join(root, "tools", "check_div_const.c"), "-o", exe,
+                    "-lm"], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert out.stdout.count(": 0 mismatches") == 3, out.stdout
