@@ -103,35 +103,59 @@ __device__ __forceinline__ double kc(double c) {
   return c;
 }
 
+// The polynomial's coefficients, read by scalar loads at their point of use
+// (IPT_TRIG_TABLE, default): kc()'s SGPR-pair constants are rematerialised
+// per use but the allocator still keeps some of them live across the loop and
+// shuffles them through VGPR lanes (v_readlane / v_writelane, VALU work).
+#ifndef IPT_TRIG_TABLE
+#define IPT_TRIG_TABLE 1
+#endif
+__constant__ double kSinCosTab[21] = {
+    0.6366197723675814,     1.5707963267948966,     6.123233995736766e-17,  // 2/pi, pi/2 hi, lo
+    2.8114572543455206e-15, -7.647163731819816e-13, 1.6059043836821613e-10, -2.505210838544172e-08,
+    2.7557319223985893e-06, -0.0001984126984126984, 0.008333333333333333,   -0.16666666666666666,
+    -1.5619206968586225e-16, 4.779477332387385e-14, -1.1470745597729725e-11, 2.08767569878681e-09,
+    -2.755731922398589e-07, 2.48015873015873e-05,   -0.001388888888888889,  0.041666666666666664,
+    -0.5,                   0.0};
+
 __device__ __forceinline__ void sincos_f(float xf, float &sf, float &cf) {
 #ifdef IPT_ABL_TRIG  // timing-only ablation build
   sf = __sinf(xf);
   cf = __cosf(xf);
   return;
 #endif
+#if IPT_TRIG_TABLE
+  int o = 0;
+  asm volatile("" : "+s"(o));  // an opaque offset: the loads stay here, not hoisted out of the loop
+  const double *T = kSinCosTab + o;
+#define IPT_KC(i, v) T[i]
+#else
+#define IPT_KC(i, v) kc(v)
+#endif
   const double x = (double)xf;
-  const double k = rint(x * kc(0.6366197723675814));
-  double r = fma(-k, kc(1.5707963267948966), x);
-  r = fma(-k, kc(6.123233995736766e-17), r);
+  const double k = rint(x * IPT_KC(0, 0.6366197723675814));
+  double r = fma(-k, IPT_KC(1, 1.5707963267948966), x);
+  r = fma(-k, IPT_KC(2, 6.123233995736766e-17), r);
   const double z = r * r;
-  double ps = kc(2.8114572543455206e-15);
-  ps = fma(ps, z, kc(-7.647163731819816e-13));
-  ps = fma(ps, z, kc(1.6059043836821613e-10));
-  ps = fma(ps, z, kc(-2.505210838544172e-08));
-  ps = fma(ps, z, kc(2.7557319223985893e-06));
-  ps = fma(ps, z, kc(-0.0001984126984126984));
-  ps = fma(ps, z, kc(0.008333333333333333));
-  ps = fma(ps, z, kc(-0.16666666666666666));
+  double ps = IPT_KC(3, 2.8114572543455206e-15);
+  ps = fma(ps, z, IPT_KC(4, -7.647163731819816e-13));
+  ps = fma(ps, z, IPT_KC(5, 1.6059043836821613e-10));
+  ps = fma(ps, z, IPT_KC(6, -2.505210838544172e-08));
+  ps = fma(ps, z, IPT_KC(7, 2.7557319223985893e-06));
+  ps = fma(ps, z, IPT_KC(8, -0.0001984126984126984));
+  ps = fma(ps, z, IPT_KC(9, 0.008333333333333333));
+  ps = fma(ps, z, IPT_KC(10, -0.16666666666666666));
   const double s = fma(ps * z, r, r);
-  double pc = kc(-1.5619206968586225e-16);
-  pc = fma(pc, z, kc(4.779477332387385e-14));
-  pc = fma(pc, z, kc(-1.1470745597729725e-11));
-  pc = fma(pc, z, kc(2.08767569878681e-09));
-  pc = fma(pc, z, kc(-2.755731922398589e-07));
-  pc = fma(pc, z, kc(2.48015873015873e-05));
-  pc = fma(pc, z, kc(-0.001388888888888889));
-  pc = fma(pc, z, kc(0.041666666666666664));
-  pc = fma(pc, z, kc(-0.5));
+  double pc = IPT_KC(11, -1.5619206968586225e-16);
+  pc = fma(pc, z, IPT_KC(12, 4.779477332387385e-14));
+  pc = fma(pc, z, IPT_KC(13, -1.1470745597729725e-11));
+  pc = fma(pc, z, IPT_KC(14, 2.08767569878681e-09));
+  pc = fma(pc, z, IPT_KC(15, -2.755731922398589e-07));
+  pc = fma(pc, z, IPT_KC(16, 2.48015873015873e-05));
+  pc = fma(pc, z, IPT_KC(17, -0.001388888888888889));
+  pc = fma(pc, z, IPT_KC(18, 0.041666666666666664));
+  pc = fma(pc, z, IPT_KC(19, -0.5));
+#undef IPT_KC
   const double c = fma(pc, z, 1.0);
   const int q = ((int)k) & 3;
   const double so = (q == 0) ? s : (q == 1) ? c : (q == 2) ? -s : -c;
@@ -938,10 +962,10 @@ struct CoopView {
 // move): lane i receives lane i-1's (shr) or lane i+1's (shl) value; lane 0
 // (shr) / lane 63 (shl) receive 0 -- callers never consume those.
 __device__ __forceinline__ float wave_shr1(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, true));
 }
 __device__ __forceinline__ float wave_shl1(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, true));
 }
 
 // Minimum of a 32-bit int over the 8 lanes of each group: three DPP stages

@@ -1285,13 +1285,17 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           // both chains in one loop (max(K) - 1 steps instead of up to twice
           // that; two independent dependency chains per step: -0.2..0.6%,
           // profiles/r03/variants_merged_r03o.log)
-          for (int s = 1; __ballot(valid && (kkp >= s || rr >= s)); ++s) {
-            const V3 N = mk((Mk.x * tv.x) * ck, (Mk.y * tv.y) * ck, (Mk.z * tv.z) * ck);
-            const V3 H = mk(A.x + B.x * S.x, A.y + B.y * S.y, A.z + B.z * S.z);
-            const V3 Nl = mk(wave_shr1(N.x), wave_shr1(N.y), wave_shr1(N.z));
-            const V3 Hr = mk(wave_shl1(H.x), wave_shl1(H.y), wave_shl1(H.z));
-            if (kkp == s) Mk = Nl;
-            if (rr == s) S = Hr;
+          const int steps = valid ? max(kkp, rr) : 0;  // this lane's chain steps
+          if (__ballot(steps > 0)) {
+            int s = 1;
+            do {  // (a do-while: the loop-carried Mk, S need no copies per step)
+              const V3 N = mk((Mk.x * tv.x) * ck, (Mk.y * tv.y) * ck, (Mk.z * tv.z) * ck);
+              const V3 H = mk(A.x + B.x * S.x, A.y + B.y * S.y, A.z + B.z * S.z);
+              const V3 Nl = mk(wave_shr1(N.x), wave_shr1(N.y), wave_shr1(N.z));
+              const V3 Hr = mk(wave_shl1(H.x), wave_shl1(H.y), wave_shl1(H.z));
+              if (kkp == s) Mk = Nl;
+              if (rr == s) S = Hr;
+            } while (__ballot(steps > s++));
           }
           if (valid) {
             V3 dLd = Mk;
