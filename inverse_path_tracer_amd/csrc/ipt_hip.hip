@@ -495,6 +495,42 @@ __device__ __forceinline__ uint32_t wave_scan_max(uint32_t v) {
 
 // TraceArgs is the kernel's FIRST parameter, so it sits at offset 0 of the
 // kernarg segment -- the in-loop reload below depends on that (IPT_ARGS_RELOAD).
+// The explicit arguments of trace_kernel as the kernarg segment holds them
+// (in order, each at its natural alignment): karg() re-reads one of them at
+// its point of use.  The adjoint's adj / grad pointers are used only by the
+// sweep and the final flush; kept live across the loop they sit in SGPRs
+// the pair loops need, and the compiler spills them to VGPR lanes and reloads
+// them (v_readlane, VALU work) after every pair block.
+struct TraceKernArgs {
+  TraceArgs a;
+  const TriIsect *isect;
+  const TriPair *pairs;
+  const TriGeom *geom;
+  const TriMat *mat;
+  const float *kd;
+  const int *emit_tri;
+  const float *emit_cdf;
+  const float *emit_pmf;
+  float *out_samples;
+  const float *adj;
+  double *grad;
+  const uint8_t *target;
+  double *edges;
+};
+static_assert(offsetof(TraceKernArgs, isect) == sizeof(TraceArgs), "pointers follow TraceArgs");
+template <typename T>
+__device__ __forceinline__ T karg(size_t off) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef __attribute__((address_space(4))) const char cst_char;
+  typedef __attribute__((address_space(4))) const T cst_t;
+  const cst_char *k = (const cst_char *)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(k));  // read here, not hoisted to the kernel's entry
+  return *(const cst_t *)(k + off);
+#else
+  (void)off;
+  return T();
+#endif
+}
 template <int MODE, bool SPEC, bool BVH>
 __global__ IPT_TRACE_BOUNDS void trace_kernel(
     const TraceArgs a, const TriIsect *__restrict__ isect, const TriPair *__restrict__ pairs,
@@ -512,10 +548,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   if (a.nscenes > 1) {
     kd += (size_t)set * 3 * a.nT;
     if (is_fwd<MODE>()) out_samples += (size_t)set * a.out_stride;
-    if (is_adj<MODE>()) {
-      adj += (size_t)set * a.adj_stride;
-      grad += (size_t)set * 3 * a.nT;
-    }
+    // (adj, grad: karg() at their uses, offset there)
   }
   const float *kdpi_g = a.kdpi_g ? a.kdpi_g + (size_t)set * 3 * a.nT : nullptr;
   constexpr int nthr = kBlock;
@@ -1193,6 +1226,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         uint32_t *swl = reinterpret_cast<uint32_t *>(lds_rec) - kBlock + (tid & ~63);
         float wx = 0.f, wy = 0.f, wz = 0.f;  // the owner's adjoint weights dL/dI / spp
         if (Kf > 0) {
+          const float *adj = karg<const float *>(offsetof(TraceKernArgs, adj)) +
+                             (a.nscenes > 1 ? (size_t)set * a.adj_stride : 0);
           const uint64_t pixel = item_pixel(a, witem);
           if (a.rc_spp != 0.f) {
             wx = adj[pixel * 3 + 0] * a.rc_spp;
@@ -1310,6 +1345,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
 #ifdef IPT_ABL_NOATOMIC  // timing-only ablation build: contributions computed, not accumulated
             if (v[0] == 12345.0) lds_acc[0] = v[1] + v[2];
 #else
+            double *grad = karg<double *>(offsetof(TraceKernArgs, grad)) + (a.nscenes > 1 ? (size_t)set * 3 * a.nT : 0);
             bins_add(sl >= 0, grad, sl >= 0 ? (size_t)sl * 3 : (size_t)tk * 3, 3, v);
 #endif
           }
@@ -1346,7 +1382,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   if (!is_fwd<MODE>()) {
     __syncthreads();
     if (n_acc > 0) {
-      double *dstp = is_adj<MODE>() ? grad : edges;
+      double *dstp = is_adj<MODE>() ? karg<double *>(offsetof(TraceKernArgs, grad)) + (a.nscenes > 1 ? (size_t)set * 3 * a.nT : 0)
+                                    : edges;
       const int nb5 = (nT + 1) * nT * kEdgeL;
       for (int i = tid; i < n_acc; i += nthr) {
         const double v = lds_acc[i];
