@@ -233,7 +233,7 @@ class Leg:
     """One workload on one scene: forward (HDR image, pixel mean fused into
     the trace kernel) and adjoint (+ gradient all-reduce) over rows [b, e)."""
 
-    def __init__(self, cx, objs, w, h, spp, mb, b=0, e=None, seed=0, step=1):
+    def __init__(self, cx, objs, w, h, spp, mb, b=0, e=None, seed=0, step=1, streams=None):
         self.cx, self.w, self.h, self.spp, self.mb, self.seed = cx, w, h, spp, mb, seed
         self.b, self.e, self.step = b, (h if e is None else e), step
         self.rows = len(range(self.b, self.e, self.step))
@@ -250,7 +250,9 @@ class Leg:
         # (the headline's Leg is the process's first: HIP maps streams onto a
         # few hardware queues in creation order, and two streams sharing one
         # run in order; measured per-share overlap: tools/pipeline_ab.py)
-        self.streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+        # (streams: reuse another Leg's pair -- the per-share pipelined table
+        # runs on the headline's streams, the process's first)
+        self.streams = list(streams) if streams else [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
         self.hdr2 = [self.hdr, torch.empty_like(self.hdr)]
         self.grad2 = [self.grad, torch.zeros_like(self.grad)]
         self.kev = []
@@ -305,6 +307,40 @@ def band_table(cx, objs, w, h, spp, mb, n=8, reps=2, interleaved=False):
     ad = [x["adj_ms"] for x in rows]
     return {"bands": rows, "fwd_max_over_mean": round(max(fw) / np.mean(fw), 4),
             "adj_max_over_mean": round(max(ad) / np.mean(ad), 4)}
+
+
+def band_table_piped(cx, objs, w, h, spp, mb, streams, n=8, reps=20):
+    """Each interleaved 1/n share of one frame with two frames in flight, the
+    headline's form (consecutive steps alternate between two streams), on the
+    headline's own streams: HIP maps streams onto its few hardware queues in
+    creation order, and two streams created late can share one and run in
+    order.  Per share: ms per step over `reps` steps (forward, adjoint) and a
+    bitwise check that the last pipelined frame equals the same frame rendered
+    alone."""
+    rows = []
+    for r in range(n):
+        b, e, st = shard_rows_interleaved(h, n, r)
+        leg = Leg(cx, objs, w, h, spp, mb, b, e, step=st, streams=streams)
+        for i in range(2):
+            leg.fwd(10**6 + i, piped=True)
+            leg.adjoint(10**6 + i, reduce=False, piped=True)
+        f = cx.timed(lambda i: leg.fwd(i, piped=True), reps, leg.streams) / reps
+        a = cx.timed(lambda i: leg.adjoint(i, reduce=False, piped=True), reps, leg.streams) / reps
+        last = leg.hdr2[(reps - 1) % 2].clone()
+        ref = torch.empty_like(last)
+        p = leg.params(reps - 1)
+        N.check(cx.L.ipt_render_dev(leg.sc.handle, C.byref(p), None, ref.data_ptr(), None, cx.st))
+        torch.cuda.synchronize(cx.dev)
+        same = bool(torch.equal(last.view(torch.int32), ref.view(torch.int32)))
+        rows.append({"rows": [b, e, st], "fwd_ms": round(f, 4), "adj_ms": round(a, 4), "bitwise_equal": same})
+        leg.close()
+    fw = [x["fwd_ms"] for x in rows]
+    ad = [x["adj_ms"] for x in rows]
+    return {"bands": rows, "reps": reps, "fwd_max_ms": max(fw), "adj_max_ms": max(ad),
+            "fwd_max_over_mean": round(max(fw) / np.mean(fw), 4), "adj_max_over_mean": round(max(ad) / np.mean(ad), 4),
+            "all_bitwise_equal": all(x["bitwise_equal"] for x in rows),
+            "workload": "interleaved 1/%d shares of the C2 frame, two frames in flight on the headline's two HIP "
+                        "streams; ms per step" % n}
 
 
 def graph_line(cx, seed=0, reps=5):
@@ -455,6 +491,7 @@ def main():
         if world == 1:
             extra["bands_c2"] = band_table(cx, CORNELL, W, H, SPP, BOUNCES, reps=4)
             extra["bands_c2_interleaved"] = band_table(cx, CORNELL, W, H, SPP, BOUNCES, reps=4, interleaved=True)
+            extra["bands_c2_piped"] = band_table_piped(cx, CORNELL, W, H, SPP, BOUNCES, head.streams)
             extra["bands_c4"] = band_table(cx, SCENE0, 1024, 1024, 256, 8, reps=1)
             extra["bands_c4_interleaved"] = band_table(cx, SCENE0, 1024, 1024, 256, 8, reps=1, interleaved=True)
             sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -516,7 +553,9 @@ def main():
             "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": "C2: CornellBox-Empty-CO.obj, 512x512, 64 spp, max_bounces=4; one frame per step "
                                    "tiled over the ranks as interleaved rows (fwd); adjoint dL/dKd of the rank's rows "
-                                   "+ RCCL all-reduce of the gradient (grad)",
+                                   "+ RCCL all-reduce of the gradient (grad); two frames in flight (consecutive steps "
+                                   "alternate between 2 HIP streams; one stream: secondary.serial)",
+                       "streams": 2 if piped_adj else "2 (fwd) / 1 (grad: gloo)",
                        "width": W, "height": H, "spp": SPP, "max_bounces": BOUNCES, "triangles": head.sc.nT,
                        "parallelism": "interleaved row tiles x%d" % world, "rank0_rows": [b, e, rs]},
             "grad_value": round(grad_value, 2), "grad_unit": "grad-Msamples/s",

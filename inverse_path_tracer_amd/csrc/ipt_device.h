@@ -119,11 +119,6 @@ __constant__ double kSinCosTab[21] = {
     -0.5,                   0.0};
 
 __device__ __forceinline__ void sincos_f(float xf, float &sf, float &cf) {
-#ifdef IPT_ABL_TRIG  // timing-only ablation build
-  sf = __sinf(xf);
-  cf = __cosf(xf);
-  return;
-#endif
 #if IPT_TRIG_TABLE
   int o = 0;
   asm volatile("" : "+s"(o));  // an opaque offset: the loads stay here, not hoisted out of the loop
@@ -864,12 +859,6 @@ __device__ __forceinline__ bool bvh_prepass(const BvhView &B, V3 p, V3 d, float 
                                             uint32_t allow = 0xffffffffu, int eidx = -1) {
   bt = __builtin_inff();
   bi = -1;
-#ifdef IPT_ABL_NOTARGET  // timing-only ablation build: no target test (wrong shadows)
-  if (SHADOW) {
-    bt = 1e30f;
-    bi = target;
-  } else
-#endif
 #ifdef IPT_BVH_STATS
   atomicAdd(&g_bvh_stats[7], 1ull);
   if (!(SHADOW && IPT_SHADOW_CULL) && !(!SHADOW && IPT_PATH_CULL && B.big_lds))
@@ -1002,7 +991,9 @@ __device__ __forceinline__ bool coop_root_test(const CoopView &C, V3 p, V3 d, fl
 }
 
 // The fp32 test of one triangle without the best-t condition (hit_test's
-// arithmetic): t if it accepts, +inf if not.
+// arithmetic): t if it accepts, +inf if not.  A NaN t (only from a NaN or
+// infinite ray) is mapped to +inf: group_lexmin orders t by its bit pattern,
+// where a negative NaN would win the group minimum and hide a real hit.
 __device__ __forceinline__ float tri_accept_t(const TriIsect &T, V3 p, V3 d) {
   const float denom = fmaf(T.n[2], d.z, fmaf(T.n[1], d.y, T.n[0] * d.x));
   const float px = p.x - T.c[0], py = p.y - T.c[1], pz = p.z - T.c[2];
@@ -1012,7 +1003,7 @@ __device__ __forceinline__ float tri_accept_t(const TriIsect &T, V3 p, V3 d) {
   const float s0 = fmaf(qz, T.e0[2], fmaf(qy, T.e0[1], fmaf(qx, T.e0[0], T.e0[3])));
   const float s1 = fmaf(qz, T.e1[2], fmaf(qy, T.e1[1], fmaf(qx, T.e1[0], T.e1[3])));
   const float s2 = fmaf(qz, T.e2[2], fmaf(qy, T.e2[1], fmaf(qx, T.e2[0], T.e2[3])));
-  const bool ok = !(fabsf(denom) < kMinDotUp) && !(t < kEpsUp) && !(s0 > 0.f) && !(s1 > 0.f) && !(s2 > 0.f);
+  const bool ok = !(fabsf(denom) < kMinDotUp) && t >= kEpsUp && !(s0 > 0.f) && !(s1 > 0.f) && !(s2 > 0.f);
   return ok ? t : __builtin_inff();
 }
 
@@ -1022,9 +1013,6 @@ __device__ __forceinline__ float tri_accept_t(const TriIsect &T, V3 p, V3 d) {
 // group stops as soon as its bi is no longer the target (occluded).
 template <bool SHADOW>
 __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3 d, float &bt, int &bi) {
-#ifdef IPT_ABL_NOTRAV  // timing-only ablation build: pre-pass only, no traversal
-  return;
-#endif
   const int lane = (int)__lane_id();
   const int g = lane >> 3, j = lane & 7;
   uint64_t M = __ballot(need);
@@ -1151,9 +1139,6 @@ __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3
 
 // Triangle::getNormal (scene_basics.h:100-109)
 __device__ __forceinline__ V3 shading_normal(const TriGeom &g, V3 q) {
-#ifdef IPT_ABL_NORMAL  // timing-only ablation build
-  return mk(g.vn[0][0], g.vn[0][1], g.vn[0][2]);
-#endif
   if (g.flags & GEOM_AXIS_FLAT) return mk(g.vn[0][0], g.vn[0][1], g.vn[0][2]);  // exact, scene_layout.h
   const V3 v0 = mk(g.v[0][0], g.v[0][1], g.v[0][2]);
   const V3 v1 = mk(g.v[1][0], g.v[1][1], g.v[1][2]);

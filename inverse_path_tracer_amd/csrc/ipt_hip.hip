@@ -886,9 +886,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         bvh_prepass<false>(bv, p, d, t, hit, -1);
         qn = coop_root_test(cv, p, d, t);
       }
-#ifndef IPT_ABL_NOTRAV_PATH  // timing-only ablation: path rays skip the tree
       coop_cast<false>(cv, qn, p, d, t, hit);
-#endif
     } else if (active) {
       if (IPT_PATH_CULL && e3)
         hit = closest_hit_pairs_culled((const lds_f32 *)lds_pr, a.pboxes, nT, p, d, t);
@@ -930,11 +928,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         while (ie < nE && !(emit_cdf[ie] >= u)) ++ie;
         ie = ie < nE ? ie : nE - 1;
         const float r1 = uniform(st), r2 = uniform(st);
-#ifdef IPT_ABL_DP  // timing-only ablation build
-        const double sq = (double)sqrtf(r1);
-#else
         const double sq = dsqrt_core((double)r1);  // r1 >= 2^-33: sqrt's identity range
-#endif
         const float ca = (float)(1.0 - sq);
         const float cb = (float)(sq * (double)(1.f - r2));
         const float cc = (float)((double)r2 * sq);
@@ -957,14 +951,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           const float ut = uniform(st);
           float cth, sth, psamp;
           if (!spec) {
-#ifdef IPT_ABL_DP
-            cth = sqrtf(ut);
-            sth = sqrtf(1.f - ut);
-#else
             cth = sqrt_core(ut);  // == (float)sqrt((double)ut) (innocuous double rounding); ut >= 2^-33
             const double omu = 1.0 - (double)ut;  // 0 or >= 2^-33
             sth = omu > 0.0 ? (float)dsqrt_core(omu) : 0.f;
-#endif
             psamp = kInvPiF;
           } else {
             const double cd = pow_d((double)ut, 1.0 / ((double)m.shininess + 1.0));
@@ -1002,9 +991,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         if (shadow && bvh_prepass<true>(bv, p, sd, ts, hs, et,
                                         a.big_pomask ? a.big_pomask[tri * nE + emitter] : 0xffffffffu, emitter))
           qn = coop_root_test(cv, p, sd, ts);
-#ifndef IPT_ABL_NOTRAV_SHADOW  // timing-only ablation: shadow rays skip the tree
         coop_cast<true>(cv, qn, p, sd, ts, hs);
-#endif
       } else if (shadow) {
         if (IPT_SHADOW_CULL && e3)
           hs = shadow_hit_pairs_small((const lds_f32 *)lds_is, pairs, a.pboxes, e3, nT, p, sd, et, ts,
@@ -1039,9 +1026,6 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
               bins_add(false, edges, bin * kEdgeW, 8, v);
             }
           } else {
-#ifdef IPT_ABL_DP
-            const float s = ((ct * ctp) / (ts * ts)) / emit_pmf[emitter];
-#else
             const double q = (double)(ct * ctp) / (td * td), pr = a.emit_pmfr[emitter];
             double s64;
             if (pr != 0.0)
@@ -1049,7 +1033,6 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             else
               s64 = q / (double)emit_pmf[emitter];
             const float s = (float)s64;
-#endif
             const V3 kee = ke3(et);
             lo = mk(kee.x * s, kee.y * s, kee.z * s);
             emit_s = s;
@@ -1214,11 +1197,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       // chunk after's (Scar) unless this is the path's first pass, and the
       // suffix at ulo goes back to the owner for its replay.
       const int Kf = MODE == MODE_ADJ ? ((finished && k > 0) ? k : 0) : ((finished && uhi > 0) ? uhi - ulo : 0);
-#ifdef IPT_ABL_NOWSWEEP  // timing-only ablation build: no backward sweep (no gradients)
-      if (0) {
-#else
       if (__ballot(Kf > 0)) {
-#endif
         const int lane = tid & 63;
         const int inc = wave_scan_add(Kf);  // inclusive scan of the task counts over the wave
         const int T = __builtin_amdgcn_readlane(inc, 63);
@@ -1342,12 +1321,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             }
             const int sl = a.grad_map ? a.grad_map[tk] : tk;
             const double v[3] = {(double)(ax * gk.x), (double)(ay * gk.y), (double)(az * gk.z)};
-#ifdef IPT_ABL_NOATOMIC  // timing-only ablation build: contributions computed, not accumulated
-            if (v[0] == 12345.0) lds_acc[0] = v[1] + v[2];
-#else
             double *grad = karg<double *>(offsetof(TraceKernArgs, grad)) + (a.nscenes > 1 ? (size_t)set * 3 * a.nT : 0);
             bins_add(sl >= 0, grad, sl >= 0 ? (size_t)sl * 3 : (size_t)tk * 3, 3, v);
-#endif
           }
           if (MODE == MODE_ADJU) {  // the suffix at the chunk's first vertex, S_lo = A + B S, back to its owner
             const V3 H = mk(A.x + B.x * S.x, A.y + B.y * S.y, A.z + B.z * S.z);
@@ -1396,11 +1371,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             j = (dst * nT + emit_tri[ie]) * kEdgeW + kEdgeL + q % 3;
           }
         }
-#ifndef IPT_ABL_NOFLUSH  // timing-only ablation build: bins never leave LDS
         if (v != 0.0) atomicAdd(dstp + j, v);
-#else
-        if (v == 12345.0) dstp[j] = v;
-#endif
       }
     }
   }
@@ -1867,15 +1838,18 @@ struct StreamScratch {
 
 // The chunk counters of a launch with `sets` material sets on stream `st`:
 // allocated and zeroed once per (stream, sets) and never reset -- each launch
-// adds exactly grabs_per_set to every set's counter (TraceArgs::chunk_base),
-// so the host returns the base this launch starts from and advances it.
-// Launches on one stream run in order; other streams get their own counters.
-// *lk holds the scene's counter lock until the caller has enqueued the launch,
-// so host threads sharing a stream enqueue in the order of their bases.
-// A launch captured into a graph (replayed without this host step) gets
-// fresh zeroed counters of its own instead (*scratch, freed behind it).
-static int stream_counters(GpuScene *s, hipStream_t st, int sets, uint32_t grabs_per_set, uint32_t **out,
-                           uint32_t *base, void **scratch, std::unique_lock<std::mutex> *lk) {
+// adds exactly grabs_per_set (launch_chunks) to every set's counter
+// (TraceArgs::chunk_base), so the host hands out the base this launch starts
+// from and, once the launch is enqueued, advances it (*cnt; a launch that
+// fails to enqueue never runs and must not move the base).  Launches on one
+// stream run in order; other streams get their own counters.  *lk holds the
+// scene's counter lock until the caller has enqueued the launch, so host
+// threads sharing a stream enqueue in the order of their bases.  A launch
+// captured into a graph (replayed without this host step) gets fresh zeroed
+// counters of its own instead (*scratch, freed behind it; *cnt = nullptr).
+static int stream_counters(GpuScene *s, hipStream_t st, int sets, uint32_t **out, uint32_t *base, void **scratch,
+                           GpuScene::Counters **cnt, std::unique_lock<std::mutex> *lk) {
+  *cnt = nullptr;
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   HIP_TRY(hipStreamIsCapturing(st, &cap));
   if (cap != hipStreamCaptureStatusNone) {
@@ -1898,8 +1872,18 @@ static int stream_counters(GpuScene *s, hipStream_t st, int sets, uint32_t grabs
   }
   *out = c->dev;
   *base = c->base;
-  c->base += grabs_per_set;  // (mod 2^32: the kernel subtracts in uint32)
+  *cnt = c;
   return 0;
+}
+
+// Chunks of a launch exactly as the kernel enumerates them (chunk_range):
+// guided instances (BVH) hand out nb chunks of c units and then chunks of
+// `small`; the others only chunks of c (they ignore chunk_small).  Each wave
+// grabs until one grab fails, so a set's counter moves by
+// max(chunks - waves, 0) + waves (TraceArgs::chunk_base).
+static uint64_t launch_chunks(bool guided, uint64_t units, uint64_t c, uint64_t small, uint64_t nb) {
+  if (!guided) return (units + c - 1) / c;
+  return nb + (units - nb * c + small - 1) / small;
 }
 
 // Guided chunk sizes (TraceArgs::chunk_big_n), BVH instances: a launch hands
@@ -1945,6 +1929,8 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
   b.chunk_base = 0;
   StreamScratch cap_ctr;  // only for a launch captured into a graph
   std::unique_lock<std::mutex> ctr_lock;  // released after the launch is enqueued
+  GpuScene::Counters *ctr = nullptr;     // advanced by `grabs` once the launch is enqueued
+  uint64_t grabs = 0;
   if (IPT_DYN_CHUNKS) {
     // ~IPT_DYN_CHUNKS_PER_WAVE chunks per wave, a multiple of 64 items, 64..4096
     const uint64_t waves = (uint64_t)(a.nscenes > 1 ? b.bps : grid) * (kBlock / 64);
@@ -1961,16 +1947,17 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
       units = a.npix;
     }
     // guided sizes: the last ~guided_tail() small chunks per wave end the launch
+    // (non-guided instances: one size, chunk_small = chunk and no big-chunk count)
     const uint64_t tail = BVH ? waves * (uint64_t)guided_tail() * small : 0;
-    const uint64_t nb = units > tail ? (units - tail) / c : 0;
+    const uint64_t nb = BVH ? (units > tail ? (units - tail) / c : 0) : 0;
+    if (!BVH) small = c;
     b.chunk = (uint32_t)c;
     b.chunk_small = (uint32_t)small;
     b.chunk_big_n = (uint32_t)nb;
-    const uint64_t chunks = nb + (units - nb * c + small - 1) / small;
-    const uint64_t grabs = (chunks > waves ? chunks - waves : 0) + waves;  // per set, see TraceArgs::chunk_base
+    const uint64_t chunks = launch_chunks(BVH, units, c, small, nb);
+    grabs = (chunks > waves ? chunks - waves : 0) + waves;  // per set, see TraceArgs::chunk_base
     cap_ctr.st = st;
-    if (stream_counters(s, st, a.nscenes, (uint32_t)grabs, &b.chunk_ctr, &b.chunk_base, &cap_ctr.p, &ctr_lock))
-      return -1;
+    if (stream_counters(s, st, a.nscenes, &b.chunk_ctr, &b.chunk_base, &cap_ctr.p, &ctr, &ctr_lock)) return -1;
   }
   StreamScratch grec;  // ADJU: the vertex-record ring (TraceArgs::grec), freed behind the launch
   if (MODE == MODE_ADJU) {
@@ -1983,6 +1970,7 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
                      s->mat, kd_dev ? kd_dev : s->kd, s->emit_tri, s->emit_cdf, s->emit_pmf, out, adj, grad, target,
                      edges);
   HIP_TRY(hipGetLastError());
+  if (ctr) ctr->base += (uint32_t)grabs;  // (mod 2^32: the kernel subtracts in uint32)
   return 0;
 }
 
@@ -2324,11 +2312,11 @@ int gpu_selftest_math(uint64_t n, uint64_t seed, uint64_t *counts_host) {
 // the brute-force loop returns the full closest hit.  Used by the exactness tests of the
 // BVH and of the shadow cull against the brute-force loop.
 // Potential-occluder mask of a shadow ray from a vertex on triangle `src`
-// towards emitter triangle `target` (all pairs when unknown: src < 0, or
-// target not an emitter -- the caller validates both).
-__device__ __forceinline__ uint32_t probe_allow(const uint32_t *masks, const int *emit_tri, int nE, int src,
+// towards emitter triangle `target` (all pairs when unknown: src outside
+// [0, nT), or target not an emitter).
+__device__ __forceinline__ uint32_t probe_allow(const uint32_t *masks, const int *emit_tri, int nE, int nT, int src,
                                                 int target) {
-  if (!masks || src < 0) return 0xffffffffu;
+  if (!masks || src < 0 || src >= nT) return 0xffffffffu;
   for (int e = 0; e < nE; ++e)
     if (emit_tri[e] == target) return masks[src * nE + e];
   return 0xffffffffu;
@@ -2420,7 +2408,7 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
     bool qn = false;
     if (valid) {
       if (target >= 0) {
-        const uint32_t allow = probe_allow(IPT_SHADOW_PO ? a.big_pomask : nullptr, emit_tri, a.nE, src, target);
+        const uint32_t allow = probe_allow(IPT_SHADOW_PO ? a.big_pomask : nullptr, emit_tri, a.nE, nT, src, target);
         if (bvh_prepass<true>(bv, p, d, t, h, target, allow)) qn = coop_root_test(cv, p, d, t);
       } else {
         bvh_prepass<false>(bv, p, d, t, h, -1);
@@ -2431,7 +2419,7 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
     coop_cast<true>(cv, qn && target >= 0, p, d, t, h);
   } else if (valid) {
     if (IPT_SHADOW_CULL && small && target >= 0) {  // the megakernel's shadow cast of small scenes
-      const uint32_t allow = probe_allow(IPT_SHADOW_PO ? a.pomask : nullptr, emit_tri, a.nE, src, target);
+      const uint32_t allow = probe_allow(IPT_SHADOW_PO ? a.pomask : nullptr, emit_tri, a.nE, nT, src, target);
       h = shadow_hit_pairs_small((const lds_f32 *)lds_is, pairs, a.pboxes, e3, nT, p, d, target, t, allow);
     } else if (IPT_PATH_CULL && small && targets && target < 0) {  // ... and its path cast
       h = closest_hit_pairs_culled((const lds_f32 *)lds_pr, a.pboxes, nT, p, d, t);

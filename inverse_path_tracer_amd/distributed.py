@@ -15,8 +15,9 @@ single-GPU result bit-for-bit (forward) or up to fp64 summation order
   rank wants the whole image); the adjoint's only exchange is ONE all-reduce
   of the nT*3 fp64 gradient (``allreduce_``), 720 B for 30 triangles --
   latency-bound on xGMI, no bucketing needed.
-* createGraph (G3) across ranks (``graph_sharded``): per-rank row-band fp64
-  bins, ONE all-reduce of the (nT+1)*nT*8 bins (59.5 KB for nT = 30), then
+* createGraph (G3) across ranks (``graph_sharded``): per-rank fp64 bins of
+  the rank's interleaved rows (as the forward and adjoint legs), ONE
+  all-reduce of the (nT+1)*nT*8 bins (59.5 KB for nT = 30), then
   DataWrapper::compress on every rank.
 * Weak scaling (bench.py): every rank renders its own frame of the same
   configuration; frame f uses the seed offset ``frame_seed`` so the global
@@ -81,19 +82,22 @@ def gather_rows(band: torch.Tensor, height: int, interleaved: bool = False) -> t
 
 def graph_sharded(scene, target, width: int, height: int, spp: int, max_bounces=None, seed: int = 0,
                   device=None):
-    """createGraph (inv_path_trace.cu:195-208) sharded by row bands: returns the
-    compressed (nT+1)*nT*7 floats, identical on every rank and equal to the
-    single-GPU result up to fp64 summation order.  `scene` is a Scene (or any
-    object with .nT and .graph(target, W, H, spp, mb, seed, row_begin, row_end)
-    returning (bins, data)).  `device` is where the all-reduce runs: default
-    CPU under gloo, the current GPU under nccl (RCCL)."""
+    """createGraph (inv_path_trace.cu:195-208) sharded by interleaved rows
+    (rank r traces rows r, r + world, ...: shard_rows_interleaved, the same
+    split as the forward and adjoint legs; contiguous bands differ in cost by
+    up to 7.6%): returns the compressed (nT+1)*nT*7 floats, identical on every
+    rank and equal to the single-GPU result up to fp64 summation order.
+    `scene` is a Scene (or any object with .nT and .graph(target, W, H, spp,
+    mb, seed, row_begin, row_end, row_step) returning (bins, data)).
+    `device` is where the all-reduce runs: default CPU under gloo, the
+    current GPU under nccl (RCCL)."""
     import numpy as np
 
     from .scene import compress
 
     W, R = world()
-    b, e = shard_rows(height, W, R)
-    bins, _ = scene.graph(target, width, height, spp, max_bounces, seed, b, e)
+    b, e, st = shard_rows_interleaved(height, W, R)
+    bins, _ = scene.graph(target, width, height, spp, max_bounces, seed, b, e, st)
     t = torch.from_numpy(np.ascontiguousarray(bins, np.float64))
     if device is None and W > 1 and dist.get_backend() == "nccl":
         device = torch.device("cuda", torch.cuda.current_device())  # RCCL reduces device tensors only

@@ -17,8 +17,12 @@ the ground-truth Kd with many more samples).
   stream (``adjoint_seed``), so the residual I - T of the forward is not
   correlated with the derivative (same-stream replay biases Adam towards
   darker albedo by O(1/spp)).
-* Scene-parallel: scene i belongs to rank i % world; per-scene parameters need
-  no collective.  ``tie_shared=k`` additionally treats the first k triangles
+* Scene-parallel: rank r owns a contiguous block of the scenes
+  (``shard_scenes``); per-scene parameters need no collective.  Every sample
+  stream is keyed on the GLOBAL scene index and the global scene count (the
+  target render of scene i, the forward / adjoint frames of step t), so a
+  split over ranks traces exactly the samples of the one-rank run: images
+  bitwise, gradients to fp64 summation order (tests/test_gpu_multirank.py).  ``tie_shared=k`` additionally treats the first k triangles
   (18 = the Cornell box, identical in every scene) as ONE parameter set shared
   by all scenes -- their gradient is summed across scenes and ranks with a
   single RCCL all-reduce per step.
@@ -53,10 +57,33 @@ class SceneTask:
     target: torch.Tensor          # target HDR image (H, W, 3)
     kd: torch.Tensor              # parameters (nT, 3)
     history: List[float] = field(default_factory=list)
+    index: int = 0                # global scene index (keys the task's sample streams)
 
 
 def _scene_files(root: str, n: int) -> List[str]:
     return [os.path.join(root, "%d.txt" % i) for i in range(n)]
+
+
+def shard_scenes(n: int, world: int, rank: int):
+    """Contiguous block [begin, end) of the n scenes owned by `rank` (balanced:
+    sizes differ by at most one).  Contiguous, so a rank's scenes of one
+    geometry are ONE batch whose sample streams continue the global ones."""
+    base, rem = divmod(n, world)
+    begin = rank * base + min(rank, rem)
+    return begin, begin + base + (1 if rank < rem else 0)
+
+
+def _runs(idx: List[int], tasks: List[SceneTask], limit: int):
+    """Split task positions into runs of consecutive global indices (<= limit each)."""
+    runs, cur = [], []
+    for i in idx:
+        if cur and (tasks[i].index != tasks[cur[-1]].index + 1 or len(cur) >= limit):
+            runs.append(cur)
+            cur = []
+        cur.append(i)
+    if cur:
+        runs.append(cur)
+    return runs
 
 
 def _geometry_key(sc: Scene) -> bytes:
@@ -65,28 +92,30 @@ def _geometry_key(sc: Scene) -> bytes:
 
 
 def build_tasks(files: List[str], width: int, height: int, target_spp: int, max_bounces: int, init: float,
-                device: torch.device, seed: int = 7, target_chunk: int = 16) -> List[SceneTask]:
+                device: torch.device, seed: int = 7, target_chunk: int = 16, first_index: int = 0) -> List[SceneTask]:
     """Load the scenes (one device geometry per distinct geometry), render the
-    targets in batches of `target_chunk`, and create the parameters."""
+    targets in batches of `target_chunk`, and create the parameters.  files[i]
+    is global scene first_index + i: its target render traces the samples of
+    seed + 10^9 + (first_index + i) * W*H*target_spp, whichever rank loads it."""
     groups = {}  # geometry key -> device Scene
     tasks = []
-    for f in files:
+    for k, f in enumerate(files):
         host = Scene.from_file(f, device=False)
         key = _geometry_key(host)
         if key not in groups:
             groups[key] = Scene.from_file(f)
         truth = torch.tensor(host.materials, device=device)
         host.close()
-        tasks.append(SceneTask(f, groups[key], truth, None, torch.full_like(truth, init).requires_grad_(True)))
+        tasks.append(SceneTask(f, groups[key], truth, None, torch.full_like(truth, init).requires_grad_(True),
+                               index=first_index + k))
     stride = width * height * target_spp
     with torch.no_grad():
         for sc in groups.values():
             mine = [i for i, t in enumerate(tasks) if t.scene is sc]
-            for c in range(0, len(mine), target_chunk):
-                idx = mine[c:c + target_chunk]
+            for idx in _runs(mine, tasks, target_chunk):
                 kd = torch.stack([tasks[i].truth for i in idx])
                 img = torch_ops.render_batch(sc, kd, width, height, target_spp, max_bounces,
-                                             seed=seed + 10**9 + idx[0] * stride, seed_stride=stride)
+                                             seed=seed + 10**9 + tasks[idx[0]].index * stride, seed_stride=stride)
                 for j, i in enumerate(idx):
                     tasks[i].target = img[j].clone()
     return tasks
@@ -99,20 +128,28 @@ class MaterialOptimizer:
     batched adjoint launch per step.  tie_shared = number of leading
     triangles whose Kd is shared by all scenes (18 = the Cornell box), or
     None.  Losses reach the tasks' histories with one device->host copy every
-    `flush_every` steps (on every rank) and at the end of each run()."""
+    `flush_every` steps (on every rank) and at the end of each run().
+
+    Sample streams: step t of the whole job (n_total scenes over all ranks,
+    default len(tasks)) traces frames [2 t n_total, 2 (t + 1) n_total) of the
+    sample-index space, scene i's forward in frame 2 t n_total + i and its
+    adjoint n_total frames later -- so each rank of a scene-parallel split
+    traces exactly the one-rank run's samples for its scenes.  A batch is
+    one geometry's tasks with consecutive global indices (seed_stride = one
+    frame between its sets)."""
 
     def __init__(self, tasks: List[SceneTask], width: int, height: int, spp: int, max_bounces: int,
                  lr: float = 1e-2, tie_shared: Optional[int] = None, seed: int = 0, flush_every: int = 16,
-                 decorrelate: bool = True):
+                 decorrelate: bool = True, n_total: Optional[int] = None):
         self.tasks, self.W, self.H, self.spp, self.mb = tasks, width, height, spp, max_bounces
         self.tie, self.seed, self.flush_every, self.decorrelate = tie_shared, seed, flush_every, decorrelate
+        self.n_total = len(tasks) if n_total is None else int(n_total)
         self.frame = width * height * spp
         self.batches = []  # (scene, tasks)
         for t in tasks:
-            for b in self.batches:
-                if b[0] is t.scene:
-                    b[1].append(t)
-                    break
+            b = self.batches[-1] if self.batches else None
+            if b is not None and b[0] is t.scene and t.index == b[1][-1].index + 1:
+                b[1].append(t)
             else:
                 self.batches.append((t.scene, [t]))
         self.leaves, self.targets, self.offsets = [], [], []
@@ -121,7 +158,7 @@ class MaterialOptimizer:
             tgt = torch.stack([t.target for t in ts])
             for j, t in enumerate(ts):
                 t.kd, t.target = leaf[j], tgt[j]
-            self.offsets.append(sum(len(b[1]) for b in self.batches[:len(self.leaves)]))
+            self.offsets.append(ts[0].index)  # global index of the batch's first scene
             self.leaves.append(leaf)
             self.targets.append(tgt)
         self.shared = None
@@ -142,7 +179,7 @@ class MaterialOptimizer:
             if self.shared is not None:
                 kd = torch.cat([self.shared.unsqueeze(0).expand(len(ts), -1, -1), leaf[:, self.tie:]], dim=1)
             # step t uses 2T frames of the sample-index space: the T forward frames, then the T adjoint frames
-            T = len(self.tasks)
+            T = self.n_total
             base = self.seed + (2 * step * T + n_before) * self.frame
             img = torch_ops.render_batch(sc, kd, self.W, self.H, self.spp, self.mb, seed=base, seed_stride=self.frame,
                                          adjoint_seed=(base + T * self.frame) if self.decorrelate else None)
@@ -176,10 +213,11 @@ class MaterialOptimizer:
 
 def optimize(tasks: List[SceneTask], width: int, height: int, spp: int, max_bounces: int, steps: int,
              lr: float = 1e-2, tie_shared: Optional[int] = None, seed: int = 0, log_every: int = 0,
-             flush_every: int = 16, decorrelate: bool = True):
+             flush_every: int = 16, decorrelate: bool = True, n_total: Optional[int] = None):
     """`steps` Adam steps of a fresh MaterialOptimizer; returns the shared
     (tied) parameter or None."""
-    m = MaterialOptimizer(tasks, width, height, spp, max_bounces, lr, tie_shared, seed, flush_every, decorrelate)
+    m = MaterialOptimizer(tasks, width, height, spp, max_bounces, lr, tie_shared, seed, flush_every, decorrelate,
+                          n_total)
     m.run(steps, log_every)
     return m.shared
 
@@ -233,13 +271,15 @@ def main():
     dev = torch.device("cuda", local)
     if ws > 1:
         dist.init_process_group("nccl", device_id=dev)
-    files = [f for i, f in enumerate(_scene_files(args.scenes, args.n)) if i % ws == rank]
+    b, e = shard_scenes(args.n, ws, rank)
+    files = _scene_files(args.scenes, args.n)[b:e]
     t0 = time.time()
-    tasks = build_tasks(files, args.width, args.height, args.target_spp, args.bounces, 0.5, dev)
+    tasks = build_tasks(files, args.width, args.height, args.target_spp, args.bounces, 0.5, dev, first_index=b)
     torch.cuda.synchronize()
     t1 = time.time()
-    optimize(tasks, args.width, args.height, args.spp, args.bounces, args.steps, args.lr,
-             tie_shared=18 if args.tie else None, log_every=10)
+    m = MaterialOptimizer(tasks, args.width, args.height, args.spp, args.bounces, args.lr,
+                          tie_shared=18 if args.tie else None, n_total=args.n)
+    m.run(args.steps, log_every=10)
     torch.cuda.synchronize()
     t2 = time.time()
     err = [float((t.kd.detach() - t.truth).abs()[18:].mean()) for t in tasks]

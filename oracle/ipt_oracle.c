@@ -1490,9 +1490,11 @@ void oro_pixel_mean(const float *samples, int64_t npix, int spp, float *hdr, uin
 /* inverse graph (inv_path_trace.cu:109-191, inv_scene.h:9-115)         */
 /* ------------------------------------------------------------------ */
 #define ACC_W 8
-/* Edge::update, inv_scene.h:26-36 (DIFFUSE components; fp64 sums) */
+/* Edge::update, inv_scene.h:26-36 (DIFFUSE components; fp64 sums); acc NULL
+ * = counting mode (oro_graph_casts: no bins) */
 static void edge_update(double *acc, int nT, int dst, int src, float w, const float pix[3],
                         const float light[3], float f0) {
+  if (!acc) return;
   double *e = acc + ((size_t)dst * nT + src) * ACC_W;
   float wf = w * f0;
   e[0] += (double)w;
@@ -1579,10 +1581,12 @@ int oro_graph_casts(void *p, int W, int H, int spp, int max_bounces, uint64_t se
     set_err("bad graph arguments");
     return -1;
   }
-  size_t na = (size_t)(sc->nT + 1) * sc->nT * ACC_W;
   int nth = nthreads();
-  double *accs = (double *)calloc(na * (size_t)nth, sizeof(double));
   uint8_t *img = (uint8_t *)calloc((size_t)W * H * 3, 1);
+  if (!img) {
+    set_err("out of memory");
+    return -1;
+  }
   int64_t b = (int64_t)row_begin * W * spp, e = (int64_t)row_end * W * spp, total = 0;
 #pragma omp parallel num_threads(nth) reduction(+ : total)
   {
@@ -1595,11 +1599,10 @@ int oro_graph_casts(void *p, int W, int H, int spp, int max_bounces, uint64_t se
     int64_t chunk = (e - b + nt - 1) / nt;
     int64_t lo = b + chunk * tid, hi = lo + chunk < e ? lo + chunk : e;
     for (int64_t g = lo; g < hi; g++)
-      trace_graph(sc, W, H, spp, max_bounces, seed, g, img, accs + na * (size_t)tid, &total);
+      trace_graph(sc, W, H, spp, max_bounces, seed, g, img, NULL, &total);  /* counting only */
   }
   *casts = total;
   free(img);
-  free(accs);
   return 0;
 }
 
@@ -1613,6 +1616,10 @@ int oro_graph(void *p, int W, int H, int spp, int max_bounces, uint64_t seed, in
   size_t na = (size_t)(sc->nT + 1) * sc->nT * ACC_W;
   int nth = nthreads();
   double *accs = (double *)calloc(na * (size_t)nth, sizeof(double));
+  if (!accs) {
+    set_err("out of memory (per-thread graph bins)");
+    return -1;
+  }
   int64_t b = (int64_t)row_begin * W * spp, e = (int64_t)row_end * W * spp;
   int64_t n = e - b;
 #pragma omp parallel num_threads(nth)

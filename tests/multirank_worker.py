@@ -1,0 +1,135 @@
+"""One rank of the product's N-rank path, started as a fresh child process by
+tests/test_gpu_multirank.py (RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in
+the environment; every rank on device 0, gloo -- the one-GPU rehearsal of the
+driver's one-rank-per-GPU RCCL run, same code path above the collective).
+
+    python tests/multirank_worker.py tile OUTDIR
+        interleaved row shares of one frame (distributed.shard_rows_interleaved):
+        fused forward through torch_ops.render_into -> gather_rows; bounded and
+        unbounded adjoints through torch_ops.adjoint_into -> allreduce_; the
+        differentiable torch_ops.render with row_step + backward -> allreduce_;
+        createGraph through distributed.graph_sharded.  Rank 0 writes tile.pt.
+    python tests/multirank_worker.py optimize OUTDIR
+        C5's scene-parallel split (optimize.shard_scenes): a contiguous block of
+        the scenes per rank, MaterialOptimizer(n_total=all scenes) for a few
+        Adam steps.  Every rank writes opt_<rank>.pt.
+
+Sizes and seeds are shared with the test through CONFIG.
+"""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+for p in (ROOT, HERE):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+# tile: a ragged frame (61 rows do not split evenly) of scenes/0.txt; the
+# north-star scene (BVH, two-kernel render) on a smaller one
+CONFIG = {"W": 64, "H": 61, "spp": 16, "mb": 4, "seed": 4242, "ns_W": 48, "ns_H": 37, "ns_spp": 8,
+          "opt_n": 4, "opt_size": 32, "opt_spp": 8, "opt_target_spp": 64, "opt_steps": 3}
+
+
+def inputs(H, W, device):
+    """The adjoint image and the createGraph target of the tile test (deterministic)."""
+    import numpy as np
+    import torch
+
+    adj = torch.from_numpy(np.random.RandomState(11).uniform(-1, 1, (H, W, 3)).astype(np.float32)).to(device)
+    target = np.random.RandomState(12).randint(0, 256, (H, W, 3)).astype(np.uint8)
+    return adj, target
+
+
+def tile(out):
+    import torch
+
+    from conftest import NORTHSTAR, SCENE0, product_scene
+    from inverse_path_tracer_amd import _native as N
+    from inverse_path_tracer_amd import torch_ops
+    from inverse_path_tracer_amd.distributed import allreduce_, gather_rows, graph_sharded, shard_rows_interleaved, world
+
+    c = CONFIG
+    Wd, R = world()
+    dev = torch.device("cuda", 0)
+    W, H, spp, mb, seed = c["W"], c["H"], c["spp"], c["mb"], c["seed"]
+    b, e, st = shard_rows_interleaved(H, Wd, R)
+    sc = product_scene(SCENE0)
+    res = {"rows": (b, e, st)}
+    adj, target = inputs(H, W, dev)
+    # forward: the rank's rows, gathered into the full image
+    p = N.make_params(W, H, spp, mb, seed, b, e, st)
+    hdr = torch.empty((p.rows, W, 3), device=dev, dtype=torch.float32)
+    torch_ops.render_into(sc, p, None, hdr)
+    torch.cuda.synchronize()
+    res["img"] = gather_rows(hdr.cpu(), H, interleaved=True)
+    # adjoints (bounded: LDS records; unbounded: the reference's estimator, global ring): one all-reduce each
+    for key, bounces in (("g_bounded", mb), ("g_unbounded", None)):
+        q = N.make_params(W, H, spp, bounces, seed, b, e, st)
+        g = torch.zeros((sc.nT, 3), device=dev, dtype=torch.float64)
+        torch_ops.adjoint_into(sc, q, None, adj.data_ptr(), g)
+        torch.cuda.synchronize()
+        res[key] = allreduce_(g.cpu())
+    # the differentiable op with row_step: forward of the share, backward through the adjoint kernel
+    kd = torch.tensor(sc.materials, device=dev, requires_grad=True)
+    img = torch_ops.render(sc, kd, W, H, spp, mb, seed, row_begin=b, row_end=e, row_step=st)
+    (img * adj[b:e:st]).sum().backward()
+    torch.cuda.synchronize()
+    res["g_autograd"] = allreduce_(kd.grad.detach().double().cpu())
+    # createGraph: interleaved rows, one all-reduce of the fp64 bins, compress on every rank
+    res["graph"] = torch.from_numpy(graph_sharded(sc, target, W, H, spp, None, seed))
+    sc.close()
+    # the BVH scene (cooperative traversal, two-kernel render): forward and adjoint shares
+    ns = product_scene(NORTHSTAR)
+    nW, nH, nspp = c["ns_W"], c["ns_H"], c["ns_spp"]
+    b2, e2, s2 = shard_rows_interleaved(nH, Wd, R)
+    p2 = N.make_params(nW, nH, nspp, mb, seed, b2, e2, s2)
+    h2 = torch.empty((p2.rows, nW, 3), device=dev, dtype=torch.float32)
+    torch_ops.render_into(ns, p2, None, h2)
+    adj2 = adj[:nH, :nW].contiguous()
+    g2 = torch.zeros((ns.nT, 3), device=dev, dtype=torch.float64)
+    torch_ops.adjoint_into(ns, p2, None, adj2.data_ptr(), g2)
+    torch.cuda.synchronize()
+    res["ns_img"] = gather_rows(h2.cpu(), nH, interleaved=True)
+    res["ns_g"] = allreduce_(g2.cpu())
+    ns.close()
+    if R == 0:
+        torch.save(res, os.path.join(out, "tile.pt"))
+
+
+def optimize(out):
+    import torch
+
+    from inverse_path_tracer_amd.distributed import world
+    from inverse_path_tracer_amd.optimize import MaterialOptimizer, _scene_files, build_tasks, shard_scenes
+
+    c = CONFIG
+    Wd, R = world()
+    dev = torch.device("cuda", 0)
+    b, e = shard_scenes(c["opt_n"], Wd, R)
+    files = _scene_files(os.path.join(ROOT, "assets", "scenes"), c["opt_n"])[b:e]
+    s = c["opt_size"]
+    tasks = build_tasks(files, s, s, c["opt_target_spp"], c["mb"], 0.5, dev, first_index=b)
+    m = MaterialOptimizer(tasks, s, s, c["opt_spp"], c["mb"], lr=1e-2, n_total=c["opt_n"])
+    m.run(c["opt_steps"])
+    torch.cuda.synchronize()
+    torch.save({t.index: {"kd": t.kd.detach().cpu(), "target": t.target.cpu(), "history": list(t.history)}
+                for t in tasks}, os.path.join(out, "opt_%d.pt" % R))
+
+
+def main():
+    import torch
+    import torch.distributed as dist
+
+    mode, out = sys.argv[1], sys.argv[2]
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo")
+    try:
+        {"tile": tile, "optimize": optimize}[mode](out)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -55,8 +55,10 @@ def _worker(rank, world, port, out, interleaved=False):
     class _OracleGraph:  # the Scene.graph calling convention over the oracle
         nT = sc.nT
 
-        def graph(self, target, w, h, spp, mb, seed, rb, re):
-            return sc.graph(w, h, spp, mb, seed, target, rb, re)
+        def graph(self, target, w, h, spp, mb, seed, rb, re, step=1):
+            # the rank's rows rb, rb + step, ... (the oracle traces contiguous bands: one per row)
+            acc = sum(sc.graph(w, h, spp, mb, seed, target, r, r + 1)[0] for r in range(rb, re, step))
+            return acc, None
 
     target = np.random.RandomState(3).randint(0, 256, (H, W, 3)).astype(np.uint8)
     data = torch.from_numpy(graph_sharded(_OracleGraph(), target, W, H, SPP, MB, SEED))

@@ -147,6 +147,31 @@ def test_adjoint_matches_oracle(scenes, name, W, H, spp, mb, seed):
     np.testing.assert_allclose(g, want, rtol=1e-9, atol=1e-12)
 
 
+def test_back_to_back_launches_with_ragged_chunks(scenes):
+    """Launches on one stream share the chunk counters, each starting from the
+    base the host advanced by the previous launch's grabs (ipt_hip.hip
+    stream_counters / launch_chunks).  509 x 97 pixels: the fused render's
+    last 8-pixel chunk holds 5 (more than its 4-pixel small chunk) and the
+    adjoint's 789 968 samples leave 80 (more than 64) past the last full
+    128-item chunk, with more chunks than waves -- a host that counted chunks
+    differently from the kernel re-traced a chunk in every later launch."""
+    P, Q = scenes["scene0"]
+    W, H, spp, mb, seed = 509, 97, 16, 4, 21
+    adj = np.random.RandomState(8).uniform(-1, 1, (H, W, 3)).astype(np.float32)
+    P.render(W, H, spp, mb, seed)             # fused render (ragged pixel chunks)
+    g1 = P.adjoint(adj, W, H, spp, mb, seed)  # ragged sample chunks
+    g2 = P.adjoint(adj, W, H, spp, mb, seed)
+    hdr = P.render(W, H, spp, mb, seed)
+    want = Q.adjoint(W, H, spp, mb, seed, adj)
+    np.testing.assert_allclose(g1, want, rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(g2, want, rtol=1e-9, atol=1e-12)
+    s, _ = Q.render_samples(W, H, spp, mb, seed)
+    import oracle_lib
+
+    hq, _ = oracle_lib.pixel_mean(s, W * H, spp)
+    assert np.array_equal(bits(hdr.reshape(-1, 3)), bits(hq))
+
+
 def test_adjoint_row_bands_sum_to_full(scenes):
     from inverse_path_tracer_amd.distributed import shard_rows
 

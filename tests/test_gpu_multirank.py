@@ -1,0 +1,133 @@
+"""The product's N-rank path on the GPU: 2 ranks, each a fresh child process
+(tests/multirank_worker.py, gloo, both on device 0), against the same work done
+by ONE rank in this process.  Samples are seeded by their global index, so the
+shares must reproduce the single-rank frame bit for bit, and the all-reduced
+gradients / graph bins must equal the single-rank sums up to fp64 summation
+order (north_star: image tiles across GPUs, one reduce of the per-material
+gradient vector).  test_distributed.py covers the same exchange with the CPU
+oracle on each rank; this is the HIP library under it."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import NORTHSTAR, SCENE0, product_scene
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+WORKER = os.path.join(HERE, "multirank_worker.py")
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _launch(mode, out, world=2, timeout=240):
+    """Start `world` ranks as child processes (never a re-exec of this one) and wait for all."""
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", WORKER, mode, str(out)], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    logs = []
+    try:
+        for p in procs:
+            o, _ = p.communicate(timeout=timeout)
+            logs.append(o.decode(errors="replace"))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, "rank %d failed (rc %s):\n%s" % (r, p.returncode, logs[r][-4000:])
+
+
+def _bits(a):
+    return np.ascontiguousarray(np.asarray(a, np.float32)).view(np.uint32)
+
+
+def test_two_rank_tiles_equal_one_rank(tmp_path):
+    from multirank_worker import CONFIG, inputs
+
+    from inverse_path_tracer_amd import _native as N
+    from inverse_path_tracer_amd import torch_ops
+
+    _launch("tile", tmp_path)
+    res = torch.load(str(tmp_path / "tile.pt"), weights_only=True)
+    c = CONFIG
+    W, H, spp, mb, seed = c["W"], c["H"], c["spp"], c["mb"], c["seed"]
+    dev = torch.device("cuda", 0)
+    adj, target = inputs(H, W, dev)
+    sc = product_scene(SCENE0)
+    # the whole frame on one rank
+    hdr = torch.empty((H, W, 3), device=dev, dtype=torch.float32)
+    torch_ops.render_into(sc, N.make_params(W, H, spp, mb, seed), None, hdr)
+    assert np.array_equal(_bits(res["img"].numpy()), _bits(hdr.cpu().numpy())), "gathered shares != one-rank frame"
+    for key, bounces in (("g_bounded", mb), ("g_unbounded", None)):
+        g = torch.zeros((sc.nT, 3), device=dev, dtype=torch.float64)
+        torch_ops.adjoint_into(sc, N.make_params(W, H, spp, bounces, seed), None, adj.data_ptr(), g)
+        np.testing.assert_allclose(res[key].numpy(), g.cpu().numpy(), rtol=1e-9, atol=1e-15, err_msg=key)
+        assert np.abs(g.cpu().numpy()).max() > 0
+    # the differentiable op returns float32 gradients: each rank's partial is rounded to float32 before the
+    # sum, so the bar is float32 rounding of the largest entry (the fp64 sums above are the exact check)
+    kd = torch.tensor(sc.materials, device=dev, requires_grad=True)
+    (torch_ops.render(sc, kd, W, H, spp, mb, seed) * adj).sum().backward()
+    want = kd.grad.double().cpu().numpy()
+    np.testing.assert_allclose(res["g_autograd"].numpy(), want, rtol=0, atol=4e-7 * np.abs(want).max())
+    # createGraph: interleaved shares, one all-reduce, compress == the one-rank graph
+    _, data = sc.graph(target, W, H, spp, None, seed)
+    np.testing.assert_allclose(res["graph"].numpy(), data, rtol=1e-6, atol=1e-7)
+    sc.close()
+    # north-star scene (BVH): forward shares bitwise, adjoint to fp64 order
+    ns = product_scene(NORTHSTAR)
+    nW, nH, nspp = c["ns_W"], c["ns_H"], c["ns_spp"]
+    h2 = torch.empty((nH, nW, 3), device=dev, dtype=torch.float32)
+    p2 = N.make_params(nW, nH, nspp, mb, seed)
+    torch_ops.render_into(ns, p2, None, h2)
+    assert np.array_equal(_bits(res["ns_img"].numpy()), _bits(h2.cpu().numpy()))
+    g2 = torch.zeros((ns.nT, 3), device=dev, dtype=torch.float64)
+    adj2 = adj[:nH, :nW].contiguous()
+    torch_ops.adjoint_into(ns, p2, None, adj2.data_ptr(), g2)
+    np.testing.assert_allclose(res["ns_g"].numpy(), g2.cpu().numpy(), rtol=1e-9, atol=1e-15)
+    ns.close()
+
+
+def test_two_rank_scene_parallel_adam_equals_one_rank(tmp_path):
+    """C5's scene-parallel split: rank r optimises a contiguous block of the
+    scenes; the targets, forward and adjoint frames are keyed on the global
+    scene index, so each scene's trajectory is the one-rank run's."""
+    from multirank_worker import CONFIG
+
+    from inverse_path_tracer_amd.optimize import MaterialOptimizer, _scene_files, build_tasks
+
+    _launch("optimize", tmp_path)
+    got = {}
+    for r in range(2):
+        got.update(torch.load(str(tmp_path / ("opt_%d.pt" % r)), weights_only=True))
+    c = CONFIG
+    n, s = c["opt_n"], c["opt_size"]
+    assert sorted(got) == list(range(n))
+    files = _scene_files(os.path.join(os.path.dirname(HERE), "assets", "scenes"), n)
+    tasks = build_tasks(files, s, s, c["opt_target_spp"], c["mb"], 0.5, torch.device("cuda", 0))
+    m = MaterialOptimizer(tasks, s, s, c["opt_spp"], c["mb"], lr=1e-2)
+    m.run(c["opt_steps"])
+    for t in tasks:
+        g = got[t.index]
+        # targets: the same samples (set b of a batch == the single-scene launch), bitwise
+        assert np.array_equal(_bits(g["target"].numpy()), _bits(t.target.cpu().numpy())), t.index
+        # losses: the same images (torch's mean over a batch of another size may round differently);
+        # later steps differ at most by the float32 rounding of gradients summed in another fp64 order
+        np.testing.assert_allclose(g["history"], t.history, rtol=1e-5)
+        np.testing.assert_allclose(g["kd"].numpy(), t.kd.detach().cpu().numpy(), rtol=0, atol=1e-6)
+        assert not np.allclose(g["kd"].numpy(), 0.5)  # the parameters moved

@@ -13,6 +13,8 @@
 #   prof         rocprofv3 --kernel-trace --stats of the C2 headline (no secondary lines)
 #   pmc          FETCH_SIZE / WRITE_SIZE passes of the C2 headline (separate runs)
 #   sq           SQ counter passes of the C2 headline
+#   attr         memory-side request classes of the C2 headline (atomics vs reads vs writes, TCC/TCP)
+#   valumix      VALU instruction-mix counter passes of the C2 headline
 #   nsprof       rocprofv3 --kernel-trace --stats of the north-star scene (BVH instances)
 #   nspmc        FETCH/WRITE + SQ counter passes of the north-star scene
 #   scenes       tools/bench_scenes.py ($SCENES, default all)
@@ -51,6 +53,12 @@ SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES
 SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE
 VALUBusy
 VALUUtilization"
+ATTR_SETS="TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_ATOMIC_sum TCC_EA0_RDREQ_sum
+TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_DRAM_sum
+TCP_TCC_ATOMIC_WITH_RET_REQ_sum TCP_TCC_ATOMIC_WITHOUT_RET_REQ_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum
+TCC_HIT_sum TCC_MISS_sum"
+MIX_SETS="SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64
+SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_MFMA_F32 SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM"
 BENCHQ=(python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-secondary)
 NS=(python3 "$R/tools/bench_scenes.py" --scenes northstar --brute-max-tris 0)
 
@@ -65,6 +73,8 @@ run() {
               -- python3 "$R/bench.py" --steps 20 --warmup 2 --no-cpu-baseline --no-secondary > "$OUT/prof_$T.log" 2>&1 ;;
     pmc) SETS=$'FETCH_SIZE\nWRITE_SIZE' pmc_passes pmc "${BENCHQ[@]}" ;;
     sq) SETS=$SQ_SETS pmc_passes sq "${BENCHQ[@]}" ;;
+    attr) SETS=$ATTR_SETS pmc_passes attr "${BENCHQ[@]}" ;;
+    valumix) SETS=$MIX_SETS pmc_passes valumix "${BENCHQ[@]}" ;;
     nsprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/nsprof_$T" -o run --output-format csv \
                 -- "${NS[@]}" --steps 10 > "$OUT/nsprof_$T.log" 2>&1 ;;
     nspmc) SETS=$'FETCH_SIZE\nWRITE_SIZE\n'"$SQ_SETS" pmc_passes nspmc "${NS[@]}" --steps 2 ;;
