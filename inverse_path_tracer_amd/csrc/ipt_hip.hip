@@ -227,13 +227,16 @@ struct TraceArgs {
   // BVH scenes: the same masks over the large-triangle pairs (nullptr = none)
   const uint32_t *big_pomask;
   // FWD with the pixel mean fused in (gpu_render, IPT_FUSED_MEAN): work comes
-  // in chunks of `chunk` (then chunk_small) launch-local pixels x spp samples;
-  // a finished sample goes to its chunk's slot in the wave's LDS (two slots
-  // per wave, mean_slot floats each, at byte mean_off of the dynamic LDS),
-  // and when the last sample of a chunk is in, the wave sums each pixel's
-  // samples in sample order (toneMap) into out_samples (HDR, npix x 3) and ldr
+  // in groups of `chunk` (then chunk_small) launch-local pixels x spp samples;
+  // each pixel of a group gets one of the wave's nslots LDS slots (spp x 3
+  // floats), a finished sample goes to its pixel's slot, and a slot whose
+  // last sample is in is summed in sample order (toneMap) into out_samples
+  // (HDR, npix x 3) and ldr.  Per wave, at byte mean_off + wave *
+  // mean_wstride * 4 of the dynamic LDS: the slots' unfinished counts
+  // [nslots], their pixels [nslots], then the slots
   int fused;
-  uint32_t mean_off, mean_slot;
+  uint32_t mean_off, mean_wstride;
+  int nslots;
   uint8_t *ldr;
 };
 static_assert(alignof(TraceArgs) == 8, "TraceArgs sits right after the ten 8-B scene pointers in the kernarg segment");
@@ -295,13 +298,6 @@ __device__ __forceinline__ void chunk_range(const TraceArgs &a, uint64_t g, uint
   }
   end = start + len < units ? start + len : units;
 }
-// MODE_FWDM: pixels of the chunk that starts at launch-local pixel lp
-template <bool GUIDED>
-__device__ __forceinline__ uint32_t fused_np(const TraceArgs &a, uint64_t lp) {
-  const uint64_t len = !GUIDED || lp < (uint64_t)a.chunk_big_n * a.chunk ? a.chunk : a.chunk_small;
-  const uint64_t left = a.npix - lp;
-  return (uint32_t)(left < len ? left : len);
-}
 
 // global pixel index (r * W + c) of this launch's work item w
 __device__ __forceinline__ uint64_t item_pixel(const TraceArgs &a, uint64_t w) {
@@ -314,6 +310,7 @@ __device__ __forceinline__ uint64_t item_pixel(const TraceArgs &a, uint64_t w) {
 }
 
 using namespace dev;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
 // Work item w of a launch -> global sample g, pixel (r, c), XORWOW state
 // after the two camera draws and the camera ray (path_trace.cu:150-165); the
@@ -717,14 +714,16 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     end = (a.n_samples * (wave + 1)) / nwaves;
   }
   bool exhausted = !dyn;
-  // fused pixel mean (MODE_FWDM): the two LDS slots' launch-local first pixel
-  // and items not yet finished; fst bit 0 = the slot being issued, bit 1 =
-  // the wave has taken its first chunk; fj = items of that slot issued so
-  // far (item j = sample j / np of pixel first + j % np, np = the chunk's
-  // pixels: sample-major inside the chunk).  Few registers: the pixel count
-  // is recomputed from the first pixel (only a launch's last chunk is short).
-  uint32_t f0lp = 0, f1lp = 0, fj = 0;
-  int fl0 = 0, fl1 = 0, fst = 1;
+  // fused pixel mean (MODE_FWDM), wave-uniform: the current group's first
+  // launch-local pixel glp, pixel count gnp and slots gslots (4 bits per
+  // pixel), fj = its samples issued so far (item j = sample j / gnp of pixel
+  // glp + j % gnp: sample-major inside the group); sfree / sdone = the ring's
+  // free slots / slots whose samples are all in but not yet summed.  A slot
+  // is held by ONE pixel, so a long path keeps one pixel's slot, not a whole
+  // chunk's: the ring also serves unbounded paths.
+  uint32_t glp = 0, gnp = 0, gslots = 0, fj = 0, sdone = 0;
+  uint32_t sfree = MODE == MODE_FWDM ? (a.nslots >= 32 ? ~0u : (1u << a.nslots) - 1u) : 0u;
+  bool started = false;
 
   bool active = false;
   Rng st;
@@ -751,6 +750,54 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   uint64_t tp_ = __builtin_amdgcn_s_memtime();
 #endif
   const int lane = tid & 63;
+  // MODE_FWDM: this wave's slot table ([nslots] unfinished counts, [nslots]
+  // pixels, padded to 16 B) and slots ([channel][sample] floats each)
+  auto fused_tab = [&](const TraceArgs &A) -> lds_u32 * {
+    return (lds_u32 *)(reinterpret_cast<char *>(lds) + A.mean_off) + (size_t)(tid >> 6) * A.mean_wstride;
+  };
+  auto fused_slots = [&](const TraceArgs &A) -> lds_f32 * {
+    return (lds_f32 *)(fused_tab(A) + ((2 * A.nslots + 3) & ~3));
+  };
+  // Sum the slots of `mask` (wave-uniform, <= 16 of them): lanes 3i + c take
+  // the i-th slot's channel c and add v_s / spp over s = 0 .. spp-1 in sample
+  // order -- toneMap's operations (path_trace.cu:186-198), i.e.
+  // pixel_mean_sm_kernel's -- then write the HDR (and 8-bit) pixel.
+  auto fused_sum = [&](const TraceArgs &A, uint32_t mask) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slots' sample writes before the sums
+    __builtin_amdgcn_wave_barrier();
+    const int m = __popc(mask);
+    const int kq = (lane * 43) >> 7, ch = lane - 3 * kq;  // lane / 3 for lane < 64
+    int slot = 0;
+    uint32_t mm = mask;
+    for (int i = 0; i < m; ++i) {  // wave-uniform: this lane's slot = the kq-th set bit
+      const int b = __builtin_ctz(mm);
+      mm &= mm - 1u;
+      slot = kq == i ? b : slot;
+    }
+    if (lane < 3 * m) {
+      const int spp = A.spp;
+      const lds_f32 *v = fused_slots(A) + (size_t)(3 * slot + ch) * spp;
+      float acc = 0.f;
+      if (A.rc_spp != 0.f && (spp & 3) == 0) {  // x * (1/spp) == x / spp (power of two); 16-B reads
+        const float rc = A.rc_spp;
+        for (int s = 0; s < spp; s += 4) {
+          const v4f w4 = *(const lds_v4 *)(v + s);
+          acc += w4.x * rc;
+          acc += w4.y * rc;
+          acc += w4.z * rc;
+          acc += w4.w * rc;
+        }
+      } else {
+        const float fs = (float)spp;
+        for (int s = 0; s < spp; ++s) acc += v[s] / fs;
+      }
+      const uint64_t px = fused_tab(A)[A.nslots + slot];
+      out_samples[px * 3 + ch] = acc;
+      if (A.ldr) A.ldr[(size_t)set * A.out_stride + px * 3 + ch] = (uint8_t)(255.f * acc / (1 + acc));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the sums' reads before the slots are refilled
+    __builtin_amdgcn_wave_barrier();
+  };
   for (;;) {
 #if defined(__HIP_DEVICE_COMPILE__)  // (the host pass has no AS4 copy)
     // The launch arguments, re-read from the kernarg segment every iteration
@@ -765,16 +812,25 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     const TraceArgs a = *apc;
 #endif
     if (MODE == MODE_FWDM) {
-      // the current chunk is fully issued and the other slot is free: the
-      // next chunk goes there (first the wave's own, then from the counter)
-      const uint32_t cn = fused_np<BVH>(a, (fst & 1) ? f1lp : f0lp) * (uint32_t)a.spp;
-      if ((!(fst & 2) || fj >= cn) && !exhausted && ((fst & 1) ? fl0 : fl1) == 0) {
+      const uint32_t G = a.chunk;  // pixels per group (the last group of a launch may hold fewer)
+      const bool issued = fj >= gnp * (uint32_t)a.spp;
+      // sum the finished slots when a group's worth is waiting, when the next
+      // group lacks free slots, or -- once the launch's work is handed out --
+      // right away (lazily: one pass sums up to 16 pixels, 3 lanes each)
+      if (sdone && ((uint32_t)__popc(sdone) >= G || exhausted || (issued && (uint32_t)__popc(sfree) < G))) {
+        fused_sum(a, sdone);
+        sfree |= sdone;
+        sdone = 0;
+      }
+      // the next group of pixels (first the wave's own, then from the counter)
+      // once the current one is fully issued and G slots are free
+      if (issued && !exhausted && (uint32_t)__popc(sfree) >= G) {
         // (a wave whose own chunk is past the end grabs once, as in the
         // unfused protocol: every wave's last grab fails, TraceArgs::chunk_base)
-        uint64_t lp0, lp1;
+        uint64_t lp0 = 0, lp1 = 0;
         bool own = false;
-        if (!(fst & 2)) {
-          fst |= 2;
+        if (!started) {
+          started = true;
           chunk_range<BVH>(a, wave, a.npix, lp0, lp1);
           own = lp0 < a.npix;
         }
@@ -784,16 +840,22 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           chunk_range<BVH>(a, nwaves + (uint32_t)__builtin_amdgcn_readfirstlane((int)c), a.npix, lp0, lp1);  // lane 0 (full exec here)
         }
         if (lp0 < a.npix) {
-          const int n = (int)(lp1 - lp0) * a.spp;
-          fst ^= 1;
-          if (fst & 1) {
-            f1lp = (uint32_t)lp0;
-            fl1 = n;
-          } else {
-            f0lp = (uint32_t)lp0;
-            fl0 = n;
-          }
+          glp = (uint32_t)lp0;
+          gnp = (uint32_t)(lp1 - lp0);
           fj = 0;
+          gslots = 0;
+          uint32_t mm = sfree;
+          for (uint32_t q = 0; q < gnp; ++q) {  // the lowest free slots, 4 bits per pixel
+            gslots |= (uint32_t)__builtin_ctz(mm) << (4 * q);
+            mm &= mm - 1u;
+          }
+          sfree = mm;
+          if ((uint32_t)lane < gnp) {  // slot table: unfinished samples, pixel
+            lds_u32 *tab = fused_tab(a);
+            const uint32_t sl = (gslots >> (4 * lane)) & 15u;
+            tab[sl] = (uint32_t)a.spp;
+            tab[a.nslots + sl] = glp + (uint32_t)lane;
+          }
         } else {
           exhausted = true;
         }
@@ -817,20 +879,18 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     // ---- refill finished lanes from the wave's range (ballot + mbcnt)
     const uint64_t need = __ballot(!active);
     if (MODE == MODE_FWDM) {
-      const uint32_t clp = (fst & 1) ? f1lp : f0lp;
-      const uint32_t np = fused_np<BVH>(a, clp);
-      const uint32_t fn = np * (uint32_t)a.spp;
-      if (need && (fst & 2) && fj < fn) {
+      const uint32_t fn = gnp * (uint32_t)a.spp;
+      if (need && fj < fn) {
         const uint32_t rank =
             __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
         if (!active && fj + rank < fn) {
           const uint32_t j = fj + rank;
-          const uint32_t s = (np & (np - 1u)) == 0u ? j >> __builtin_ctz(np) : j / np;
-          const uint32_t q = j - s * np;
+          const uint32_t s = (gnp & (gnp - 1u)) == 0u ? j >> __builtin_ctz(gnp) : j / gnp;
+          const uint32_t q = j - s * gnp;
           int r, c;
-          item_ray_ls(a, seed, clp + q, s, st, p, d, r, c);
-          // the sample's LDS place: slot fst & 1, [pixel q][channel][sample s]
-          witem = (uint64_t)(q * 3u * (uint32_t)a.spp + s) | ((uint64_t)(fst & 1) << 31);
+          item_ray_ls(a, seed, glp + q, s, st, p, d, r, c);
+          // the sample's LDS place: its pixel's slot, sample s
+          witem = (uint64_t)((gslots >> (4 * q)) & 15u) | ((uint64_t)s << 4);
           L = mk(0.f, 0.f, 0.f);
           Le = L;
           Ld = L;
@@ -871,7 +931,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       next += (uint64_t)__popcll(need);
     }
     PHASE(0)
-    if (__ballot(active) == 0) break;
+    // (MODE_FWDM: the last finished slots are summed at the loop top first)
+    if (__ballot(active) == 0 && (MODE != MODE_FWDM || (exhausted && sdone == 0 && fj >= gnp * (uint32_t)a.spp)))
+      break;
 #ifdef IPT_PHASE_TIMING
     tacc[6] += 1;
     tacc[7] += __popcll(__ballot(active));
@@ -1109,10 +1171,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     bool ufirst = false;
     if (finished) {
       active = false;
-      if (MODE == MODE_FWDM) {
-        float *o = reinterpret_cast<float *>(reinterpret_cast<char *>(lds) + a.mean_off) +
-                   (size_t)(tid >> 6) * 2 * a.mean_slot + ((witem >> 31) ? a.mean_slot : 0u) +
-                   (uint32_t)(witem & 0x7fffffffu);
+      if (MODE == MODE_FWDM) {  // slot [channel][sample]
+        lds_f32 *o = fused_slots(a) + (uint32_t)(witem & 15u) * 3u * (uint32_t)a.spp + (uint32_t)(witem >> 4);
         o[0] = L.x;
         o[a.spp] = L.y;
         o[2 * a.spp] = L.z;
@@ -1131,52 +1191,22 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         ulo = uhi > vmax ? uhi - vmax : 0;
       }
     }
-    if (MODE == MODE_FWDM) {
-      // fused pixel mean: count the finished samples per slot; a slot whose
-      // last sample came in is summed now (toneMap, path_trace.cu:186-198:
-      // per pixel, per channel, v_s / spp added in sample order -- the same
-      // float operations as pixel_mean_sm_kernel) by lanes 3q + c, then freed
-      const uint64_t fm = __ballot(finished);
-      if (fm) {
-        const int n1 = __popcll(__ballot(finished && (witem >> 31) != 0));
-        const int n0 = __popcll(fm) - n1;
-        fl0 -= n0;
-        fl1 -= n1;
-        const bool red0 = n0 > 0 && fl0 == 0, red1 = n1 > 0 && fl1 == 0;
-        if (red0 || red1) {
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slot's sample writes before the sums
-          __builtin_amdgcn_wave_barrier();
-          const int spp = a.spp;
-          const lds_f32 *wbase = (const lds_f32 *)(reinterpret_cast<char *>(lds) + a.mean_off) +
-                                 (size_t)(tid >> 6) * 2 * a.mean_slot;
-          for (int x = 0; x < 2; ++x) {  // wave-uniform
-            if (!(x ? red1 : red0)) continue;
-            const int np = (int)fused_np<BVH>(a, x ? f1lp : f0lp);
-            if (lane < 3 * np) {
-              const int q = (lane * 43) >> 7, ch = lane - 3 * q;  // lane / 3 for lane < 64
-              const lds_f32 *v = wbase + (x ? a.mean_slot : 0u) + (size_t)(3 * q + ch) * spp;
-              float acc = 0.f;
-              if (a.rc_spp != 0.f && (spp & 3) == 0) {  // x * (1/spp) == x / spp (power of two); 16-B reads
-                const float rc = a.rc_spp;
-                for (int s = 0; s < spp; s += 4) {
-                  const v4f w4 = *(const lds_v4 *)(v + s);
-                  acc += w4.x * rc;
-                  acc += w4.y * rc;
-                  acc += w4.z * rc;
-                  acc += w4.w * rc;
-                }
-              } else {
-                const float fs = (float)spp;
-                for (int s = 0; s < spp; ++s) acc += v[s] / fs;
-              }
-              const uint64_t px = (uint64_t)(x ? f1lp : f0lp) + (uint64_t)q;
-              out_samples[px * 3 + ch] = acc;
-              if (a.ldr) a.ldr[(size_t)set * a.out_stride + px * 3 + ch] = (uint8_t)(255.f * acc / (1 + acc));
-            }
-          }
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the sums' reads before the slot is refilled
-          __builtin_amdgcn_wave_barrier();
-        }
+    if (MODE == MODE_FWDM && __ballot(finished)) {
+      // fused pixel mean: each finished lane counts its sample off its slot's
+      // table entry (LDS atomic, after the wave's sample writes: a wave's LDS
+      // operations complete in order); the lane that takes a count to zero
+      // marks the slot done.  Slots are summed lazily at the loop top.
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      uint32_t left = 0;
+      if (finished)
+        left = __hip_atomic_fetch_sub(fused_tab(a) + (uint32_t)(witem & 15u), 1u, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+      uint64_t comp = __ballot(finished && left == 1u);
+      while (comp) {  // wave-uniform: usually 0 or 1 slot per iteration
+        const int l = (int)__builtin_ctzll(comp);
+        comp &= comp - 1ull;
+        sdone |= 1u << (__builtin_amdgcn_readlane((int)(witem & 15u), l) & 31);
       }
     }
     if (is_adj<MODE>()) {
@@ -1775,7 +1805,8 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.rc_H = (p.height > 0 && (p.height & (p.height - 1)) == 0) ? 1.0f / (float)p.height : 0.f;
   a.fused = 0;
   a.mean_off = 0;
-  a.mean_slot = 0;
+  a.mean_wstride = 0;
+  a.nslots = 0;
   a.ldr = nullptr;
   return a;
 }
@@ -2098,27 +2129,38 @@ int gpu_pixel_mean_sm(const float *samples_dev, int64_t npix, int spp, float *hd
   return pixel_mean_sm_sets(samples_dev, npix, spp, 1, hdr_dev, ldr_dev, stream);
 }
 
-// Fused pixel mean (IPT_FUSED_MEAN): pixels per chunk, or 0 when the launch
-// renders through the sample buffer + pixel_mean_sm_kernel instead.  A chunk
-// holds p pixels x spp samples with p * spp <= 256 (p a power of two <= 16,
-// so the 3p summing lanes fit a wave): two LDS slots of 3 KB at most per wave.
-// Bounded paths only (a path longer than a chunk's issue time stalls the
-// wave's refill until its slot is summed); the index math needs < 2^32
-// samples per frame.  IPT_RENDER_TWO_KERNEL=1 (environment) forces the
+// Fused pixel mean (IPT_FUSED_MEAN): the ring of one-pixel slots per wave
+// (nslots, <= 16, spp x 3 floats each, IPT_FUSED_WAVE_BYTES of LDS per wave)
+// and the pixels per group (a power of two, group x spp <= 256 samples, >= 32),
+// or {0, 0} when the launch renders through the sample
+// buffer + pixel_mean_sm_kernel instead.  A pixel's slot stays busy until its
+// last sample is in, so the ring holds at least two groups (bounded paths of
+// <= 8 bounces) or four (longer or unbounded paths: a few long paths then
+// still leave the next groups their slots -- simulated lane use >= 99% for
+// the reference's Russian roulette).  The index math needs
+// < 2^32 samples per frame.  IPT_RENDER_TWO_KERNEL=1 (environment) forces the
 // unfused path (A/B timing, tests).
 #ifndef IPT_FUSED_MEAN
 #define IPT_FUSED_MEAN 1
 #endif
-#ifndef IPT_FUSED_MAX_BOUNCES
-#define IPT_FUSED_MAX_BOUNCES 16
+#ifndef IPT_FUSED_WAVE_BYTES
+#define IPT_FUSED_WAVE_BYTES 6144
 #endif
-static int fused_pixels(const RenderParams &p) {
-  if (!IPT_FUSED_MEAN || !IPT_DYN_CHUNKS || std::getenv("IPT_RENDER_TWO_KERNEL")) return 0;
-  if (p.max_bounces < 0 || p.max_bounces > IPT_FUSED_MAX_BOUNCES || p.spp > 256) return 0;
-  if ((uint64_t)p.width * (uint64_t)p.height * (uint64_t)p.spp > 0xffffffffull) return 0;
-  int q = 1;
-  while (q < 16 && 2 * q * p.spp <= 256) q *= 2;
-  return q * p.spp >= 64 ? q : 0;
+struct FusedShape {
+  int slots, group;
+};
+static FusedShape fused_shape(const RenderParams &p) {
+  const FusedShape none = {0, 0};
+  if (!IPT_FUSED_MEAN || !IPT_DYN_CHUNKS || std::getenv("IPT_RENDER_TWO_KERNEL")) return none;
+  if ((uint64_t)p.width * (uint64_t)p.height * (uint64_t)p.spp > 0xffffffffull || p.spp > 256) return none;
+  const int slots = std::min(16, IPT_FUSED_WAVE_BYTES / (12 * p.spp));
+  const bool long_paths = p.max_bounces < 0 || p.max_bounces > 8;
+  const int cap = slots / (long_paths ? 4 : 2);  // groups the ring holds at once
+  if (cap < 1) return none;
+  int g = 1;
+  while (2 * g <= cap && 2 * g * p.spp <= 256) g *= 2;
+  if (g * p.spp < 32) return none;  // (tiny spp: a grab per few samples; the two-kernel render wins)
+  return {slots, g};
 }
 
 int gpu_render(GpuScene *s, const RenderParams &p, const float *kd_dev, float *hdr_dev, uint8_t *ldr_dev,
@@ -2130,14 +2172,16 @@ int gpu_render(GpuScene *s, const RenderParams &p, const float *kd_dev, float *h
   // the wave's rays spread over 64 pixels (a chunk's p <= 16 pixels put many
   // lanes into the tree at once) and the slots cost the tree's LDS stage
   // residency -- north-star 3.92 -> 4.60 ms fused (profiles/r03/fusedab_r03h.log)
-  if (const int fp = use_bvh(s) ? 0 : fused_pixels(p)) {
+  const FusedShape fs = use_bvh(s) ? FusedShape{0, 0} : fused_shape(p);
+  if (fs.group > 0) {
     TraceArgs a = make_args(s, p);
     a.fused = 1;
-    a.chunk = (uint32_t)fp;  // pixels per (big) chunk; launch_inst adds the small ones
-    a.mean_slot = (uint32_t)(3 * fp * p.spp);
+    a.chunk = (uint32_t)fs.group;  // pixels per group; launch_inst may halve it for thin launches
+    a.nslots = fs.slots;
+    a.mean_wstride = (uint32_t)(((2 * fs.slots + 3) & ~3) + 3 * fs.slots * p.spp + 3) & ~3u;  // floats per wave
     a.ldr = ldr_dev;
     a.out_stride = (uint64_t)npix * 3;  // per material set: its own HDR (and LDR) image
-    const size_t tail = (size_t)(kBlock / 64) * 2 * a.mean_slot * sizeof(float);
+    const size_t tail = (size_t)(kBlock / 64) * a.mean_wstride * sizeof(float);
     return launch<MODE_FWDM>(s, a, table_bytes(a), kd_dev, hdr_dev, nullptr, nullptr, nullptr, nullptr,
                              (hipStream_t)stream, tail);
   }

@@ -1,17 +1,19 @@
 """The forward with the pixel mean fused into the trace kernel (gpu_render,
-MODE_FWDM): each wave sums its chunks' samples from LDS in sample order, so
-the HDR image (and its 8-bit tonemap) must be bit-identical to the oracle's
-toneMap over the oracle's per-sample radiances (path_trace.cu:186-198) and to
-the unfused two-kernel render (IPT_RENDER_TWO_KERNEL=1: sample buffer +
+MODE_FWDM): each wave keeps a ring of one-pixel LDS slots and sums a pixel's
+samples in sample order once its last one is in, so the HDR image (and its
+8-bit tonemap) must be bit-identical to the oracle's toneMap over the
+oracle's per-sample radiances (path_trace.cu:186-198) and to the unfused
+two-kernel render (IPT_RENDER_TWO_KERNEL=1: sample buffer +
 pixel_mean_sm_kernel).
 
-Cases cover the chunk shapes gpu_render picks (pixels per chunk p with
-p * spp <= 256): spp a power of two (16-B LDS reads, multiply by 1/spp), spp
-not a power of two (IEEE division), spp = 256 (one pixel per chunk), partial
-last chunks (1 and 3 pixels: the division path of the item split), the
-longest bounded paths it accepts (16 bounces), row bands and interleaved
-shares, the BVH instance, and the unfused fallbacks (spp * 16 < 64,
-unbounded paths)."""
+Cases cover the group shapes gpu_render picks (p pixels per group, p * spp
+<= 256, the ring holding 2 groups for <= 8 bounces and 4 otherwise): spp a
+power of two (16-B LDS reads, multiply by 1/spp), spp not a power of two
+(IEEE division), spp = 256 (one pixel per group), partial last groups (the
+division path of the item split), long bounded paths and the reference's
+own unbounded estimator (long Russian-roulette paths hold their pixel's slot
+while the ring moves on), row bands and interleaved shares, the BVH
+instance (two-kernel render) and the unfused fallback (spp > 256)."""
 import os
 
 import numpy as np
@@ -52,12 +54,16 @@ def two_kernel(fn):
 @pytest.mark.parametrize("name,W,H,spp,mb,seed", [
     ("cornell", 33, 17, 5, 4, 7),       # p = 16, spp odd (division); last chunk 1 pixel
     ("scene0", 31, 7, 64, 4, 3),        # p = 4 (the C2 shape); last chunk 1 pixel
-    ("scene0", 37, 3, 48, 16, 2),       # 16 bounces (the fused limit); last chunk 3 pixels
+    ("scene0", 37, 3, 48, 16, 2),       # 16 bounces (long paths: 4 groups in the ring); last group 3 pixels
+    ("scene0", 29, 11, 48, 40, 12),     # 40 bounces
     ("scene0", 20, 10, 100, 2, 9),      # the reference's 100 spp: p = 2
     ("scene0", 9, 5, 256, 8, 1),        # p = 1
     ("northstar", 24, 20, 16, 4, 11),   # BVH instance, p = 16
-    ("scene0", 16, 8, 2, 4, 4),         # unfused fallback: 16 pixels x 2 spp < 64 items
-    ("scene0", 16, 8, 8, None, 4),      # unfused fallback: unbounded paths
+    ("scene0", 16, 8, 2, 4, 4),         # unfused fallback: 8 pixels x 2 spp < 32 samples per group
+    ("scene0", 16, 8, 8, None, 4),      # unbounded paths (the reference's estimator)
+    ("cornell", 45, 23, 64, None, 6),   # unbounded, 64 spp: 8 slots, 2-pixel groups
+    ("scene0", 31, 13, 100, None, 8),   # unbounded, the reference's 100 spp: 5 slots, 1-pixel groups
+    ("scene0", 7, 3, 300, 4, 2),        # unfused fallback: spp > 256
 ])
 def test_fused_render_equals_oracle_tonemap(scenes, oracle, name, W, H, spp, mb, seed):
     P, Q = scenes[name]
@@ -80,6 +86,17 @@ def test_fused_c2_frame_equals_oracle_and_unfused(scenes, oracle):
     for r in (0, 5):
         share = P.render(512, 512, 64, 4, 0, r, 512, row_step=8)
         assert np.array_equal(bits(share), bits(hdr[r::8]))
+
+
+def test_fused_unbounded_reference_config_equals_oracle(scenes, oracle):
+    """The legacy createImage configuration (scenes/0.txt, 500x500, 100 spp,
+    no bounce cap, path_trace.cu:200-234) through the fused ring: == the
+    oracle's toneMap bitwise (HDR and 8-bit), with no per-sample buffer."""
+    P, Q = scenes["scene0"]
+    hdr, u8 = P.render(500, 500, 100, None, 77, ldr=True)
+    want, uq, _ = Q.render(500, 500, 100, None, 77)
+    assert np.array_equal(bits(hdr), bits(want))
+    assert np.array_equal(u8, uq)
 
 
 def test_fused_band_of_c4_shape(scenes):

@@ -98,7 +98,7 @@ def main():
         pr8 = N.make_params(512, 512, 64, 4, 0, 0, 512, 8)  # one interleaved 1/8 share (the bench's tile split)
         hdr = torch.empty((512 * 512, 3), device=dev)
         pu = N.make_params(512, 512, 64, None, 0)  # the reference's own estimator (no bounce cap)
-        kinds = ("fwd", "fsm", "adj", "band", "render", "render8", "adj8", "adju")
+        kinds = ("fwd", "fsm", "adj", "band", "render", "render8", "adj8", "adju", "renderu")
         times = {n: {k: [] for k in kinds} for n in libs}
         for rnd in range(6):
             for n, L in libs.items():
@@ -114,8 +114,8 @@ def main():
                             assert L.ipt_render_samples_sm_dev(hs[n], C.byref(p), None, buf.data_ptr(), st) == 0
                         elif kind == "band":
                             assert L.ipt_render_samples_sm_dev(hs[n], C.byref(pb), None, buf.data_ptr(), st) == 0
-                        elif kind in ("render", "render8"):
-                            pp = p if kind == "render" else pr8
+                        elif kind in ("render", "render8", "renderu"):
+                            pp = {"render": p, "render8": pr8, "renderu": pu}[kind]
                             assert L.ipt_render_dev(hs[n], C.byref(pp), None, hdr.data_ptr(), None, st) == 0
                         elif kind == "adju":
                             assert L.ipt_adjoint_dev(hs[n], C.byref(pu), None, adj.data_ptr(), g.data_ptr(), st) == 0
@@ -136,6 +136,7 @@ def main():
                                     "render8_ms": round(float(np.median(times[n]["render8"])), 4),
                                     "adj8_ms": round(float(np.median(times[n]["adj8"])), 4),
                                     "adju_ms": round(float(np.median(times[n]["adju"])), 4),
+                                    "renderu_ms": round(float(np.median(times[n]["renderu"])), 4),
                                     "fwd_Msps": round(512 * 512 * 64 / f / 1e3, 1), "adj_Msps": round(512 * 512 * 64 / a / 1e3, 1)}
             print(sname, n, out[sname + ":" + n], flush=True)
     print(json.dumps(out))
