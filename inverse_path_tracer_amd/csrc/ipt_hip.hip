@@ -97,9 +97,13 @@ __host__ __device__ inline size_t graph_lds_doubles(int nT, int nE) {
   return (size_t)(nT + 1) * nT * kEdgeL + (size_t)(nT + 1) * (nE > 0 ? nE : 0) * 3;
 }
 constexpr int kMaxAdjBounces = 62;
-// ADJU ring slots per lane, in global memory (TraceArgs::grec: 3 words x 64
-// slots x the grid's lanes, 251 MB at C3, stream-ordered scratch; the
-// records of the live vertices stay in L2 / MALL).  Paths of more than 64
+// ADJU ring slots per lane, in global memory (TraceArgs::grec: 6 words --
+// tri | et, emitter factor, coeff, and the prefix throughput M_k -- x 64
+// slots x the grid's lanes: 503 MB at C3 for 327 680 resident lanes,
+// stream-ordered scratch; a lane's live records are its current path's, so
+// the touched lines are a few slots per lane).  Smaller rings cost replays:
+// 16 slots +5% / +10% / +6% and 8 slots +13% / +27% / +23% on Cornell /
+// scenes/0 / north-star (profiles/r04/variants_trishade_ring_occ_chunk_r04c.log).  Paths of more than 64
 // vertices replay their earlier chunks (a path of K vertices costs about
 // K^2 / 128 extra vertex traces).  Round 2 kept an 8-slot ring in LDS (24 KB
 // per workgroup): every path longer than 8 vertices replayed, C3 unbounded
@@ -238,8 +242,37 @@ struct TraceArgs {
   uint32_t mean_off, mean_wstride;
   int nslots;
   uint8_t *ldr;
+  // XCD regions (ADJ, ADJU, GRAPH; one material set): the launch's rows are
+  // split into nreg interleaved sets (launch row lr -> region lr % nreg) and
+  // block b traces region b % nreg only -- the dispatcher deals blocks
+  // round-robin over the 8 XCDs, so a region's pixels (adjoint image, target
+  // image) are read into ONE XCD's L2 instead of all eight (placement only
+  // changes speed, never a result).  Region r is the launch with row0 =
+  // reg_row0[r], row_step * nreg, reg_npix[r] pixels (Lemire constant
+  // reg_m_npix[r]), its own chunk counter (chunk_ctr[r]) and base, and
+  // reg_nb[r] big chunks (guided instances).
+  int nreg;
+  int reg_row0[8];
+  uint32_t reg_base[8], reg_nb[8];
+  uint64_t reg_npix[8], reg_m_npix[8];
 };
 static_assert(alignof(TraceArgs) == 8, "TraceArgs sits right after the ten 8-B scene pointers in the kernarg segment");
+
+// TraceArgs as region `reg` sees it (TraceArgs::nreg); the per-region
+// fields are read through `src`, the kernarg segment's copy (scalar loads with
+// a wave-uniform offset -- indexing a register copy of the arrays miscompiles)
+template <class SRC>
+__device__ __forceinline__ void region_view(TraceArgs &v, const SRC *src, int reg) {
+  if (v.nreg > 1) {
+    v.row0 = src->reg_row0[reg];
+    v.row_step *= v.nreg;
+    v.npix = src->reg_npix[reg];
+    v.n_samples = v.npix * (uint64_t)v.spp;
+    v.m_npix = src->reg_m_npix[reg];
+    v.chunk_base = src->reg_base[reg];
+    v.chunk_big_n = src->reg_nb[reg];
+  }
+}
 
 __device__ __forceinline__ uint32_t udiv32(uint32_t n, uint64_t m, uint32_t d) {
   return d == 1u ? n : (uint32_t)__umul64hi(m, (uint64_t)n);
@@ -695,8 +728,20 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   }
   {  // the wave's persistent loop
   // wave-uniform sample range (static partition, regenerated per lane)
-  const uint32_t wave = __builtin_amdgcn_readfirstlane((sblock * kBlock + tid) >> 6);
-  const uint32_t nwaves = (sgrid * kBlock) >> 6;
+  // XCD region (TraceArgs::nreg) of this block, and the wave's index among
+  // the region's waves
+  const int nreg = a.nreg > 1 ? a.nreg : 1;
+  const int reg = nreg > 1 ? (int)(sblock & (uint32_t)(nreg - 1)) : 0;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(((sblock / (uint32_t)nreg) * kBlock + tid) >> 6);
+  const uint32_t nwaves = ((sgrid / (uint32_t)nreg) * kBlock) >> 6;
+  TraceArgs ar = a;
+#if defined(__HIP_DEVICE_COMPILE__)
+  {
+    typedef __attribute__((address_space(4))) const TraceArgs cst_args0;
+    const cst_args0 *k0 = (const cst_args0 *)__builtin_amdgcn_kernarg_segment_ptr();  // TraceArgs is at offset 0
+    region_view(ar, k0, reg);
+  }
+#endif
   // Work items w in [0, n_samples) of this launch (item_split): pixel-major
   // w = lp * spp + s, or sample-major w = s * npix + lp over the launch's
   // pixels lp.  Either way the sample's seed is seed + its global index g:
@@ -708,10 +753,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   const bool dyn = a.chunk != 0;
   uint64_t next, end;
   if (dyn) {
-    chunk_range<BVH>(a, wave, a.n_samples, next, end);
+    chunk_range<BVH>(ar, wave, ar.n_samples, next, end);
   } else {
-    next = (a.n_samples * wave) / nwaves;
-    end = (a.n_samples * (wave + 1)) / nwaves;
+    next = (ar.n_samples * wave) / nwaves;
+    end = (ar.n_samples * (wave + 1)) / nwaves;
   }
   bool exhausted = !dyn;
   // fused pixel mean (MODE_FWDM), wave-uniform: the current group's first
@@ -809,7 +854,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     typedef __attribute__((address_space(4))) const TraceArgs cst_args;
     const cst_args *apc = (const cst_args *)__builtin_amdgcn_kernarg_segment_ptr();  // first parameter: offset 0
     asm volatile("" : "+s"(apc));
-    const TraceArgs a = *apc;
+    TraceArgs a = *apc;
+    region_view(a, apc, reg);
+#else
+    TraceArgs a = ar;
 #endif
     if (MODE == MODE_FWDM) {
       const uint32_t G = a.chunk;  // pixels per group (the last group of a launch may hold fewer)
@@ -865,7 +913,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       // (profiles/r02_variants_chunk_*.log): 8 counters on separate lines
       // with stealing and a grab prefetched one chunk ahead were both slower.
       uint32_t c = 0;
-      if (lane == 0) c = atomicAdd(a.chunk_ctr + set, 1u) - a.chunk_base;
+      if (lane == 0) c = atomicAdd(a.chunk_ctr + set + reg, 1u) - a.chunk_base;
       c = (uint32_t)__shfl((int)c, 0);
       uint64_t start, stop;
       chunk_range<BVH>(a, nwaves + c, a.n_samples, start, stop);
@@ -1535,9 +1583,9 @@ struct GpuScene {
   // advanced by every launch by a known amount (TraceArgs::chunk_base)
   struct Counters {
     hipStream_t stream;
-    int sets;
+    int words;
     uint32_t *dev;
-    uint32_t base;
+    std::vector<uint32_t> base;  // per counter word
   };
   std::vector<Counters> counters;
   std::mutex counters_mu;
@@ -1804,6 +1852,12 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.rc_W = (p.width > 0 && (p.width & (p.width - 1)) == 0) ? 1.0f / (float)p.width : 0.f;
   a.rc_H = (p.height > 0 && (p.height & (p.height - 1)) == 0) ? 1.0f / (float)p.height : 0.f;
   a.fused = 0;
+  a.nreg = 1;
+  for (int r = 0; r < 8; ++r) {
+    a.reg_row0[r] = 0;
+    a.reg_base[r] = a.reg_nb[r] = 0;
+    a.reg_npix[r] = a.reg_m_npix[r] = 0;
+  }
   a.mean_off = 0;
   a.mean_wstride = 0;
   a.nslots = 0;
@@ -1878,33 +1932,58 @@ struct StreamScratch {
 // threads sharing a stream enqueue in the order of their bases.  A launch
 // captured into a graph (replayed without this host step) gets fresh zeroed
 // counters of its own instead (*scratch, freed behind it; *cnt = nullptr).
-static int stream_counters(GpuScene *s, hipStream_t st, int sets, uint32_t **out, uint32_t *base, void **scratch,
-                           GpuScene::Counters **cnt, std::unique_lock<std::mutex> *lk) {
+// `words` counter words: one per material set (scene batch) or per XCD
+// region (TraceArgs::nreg); *cnt->base[w] is word w's value when this launch
+// starts (all zero for a captured launch, *cnt = the capture's throwaway).
+static int stream_counters(GpuScene *s, hipStream_t st, int words, uint32_t **out, void **scratch,
+                           GpuScene::Counters **cnt, GpuScene::Counters *cap_cnt, std::unique_lock<std::mutex> *lk) {
   *cnt = nullptr;
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   HIP_TRY(hipStreamIsCapturing(st, &cap));
   if (cap != hipStreamCaptureStatusNone) {
-    HIP_TRY(hipMallocAsync(scratch, (size_t)sets * sizeof(uint32_t), st));
-    HIP_TRY(hipMemsetAsync(*scratch, 0, (size_t)sets * sizeof(uint32_t), st));
+    HIP_TRY(hipMallocAsync(scratch, (size_t)words * sizeof(uint32_t), st));
+    HIP_TRY(hipMemsetAsync(*scratch, 0, (size_t)words * sizeof(uint32_t), st));
     *out = (uint32_t *)*scratch;
-    *base = 0;
+    cap_cnt->words = words;
+    cap_cnt->base.assign((size_t)words, 0u);
+    *cnt = cap_cnt;
     return 0;
   }
   *lk = std::unique_lock<std::mutex>(s->counters_mu);
   GpuScene::Counters *c = nullptr;
   for (auto &e : s->counters)
-    if (e.stream == st && e.sets == sets) c = &e;
+    if (e.stream == st && e.words == words) c = &e;
   if (!c) {
     uint32_t *dev = nullptr;
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&dev), (size_t)sets * sizeof(uint32_t)));
-    HIP_TRY(hipMemset(dev, 0, (size_t)sets * sizeof(uint32_t)));
-    s->counters.push_back({st, sets, dev, 0u});
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&dev), (size_t)words * sizeof(uint32_t)));
+    HIP_TRY(hipMemset(dev, 0, (size_t)words * sizeof(uint32_t)));
+    s->counters.push_back({st, words, dev, std::vector<uint32_t>((size_t)words, 0u)});
     c = &s->counters.back();
   }
   *out = c->dev;
-  *base = c->base;
   *cnt = c;
   return 0;
+}
+
+// XCD regions of a launch (TraceArgs::nreg) for the integrators that read a
+// per-pixel input image (adjoint, createGraph), one material set: measured
+// (profiles/r04/envab_regions_r04f.log) they cut the C2 adjoint's fetched
+// bytes 25.9 -> 3.8 MB per launch -- every XCD's L2 no longer pulls the whole
+// adjoint image -- but cost 1.6% time (C2 adjoint 1.911 -> 1.942 ms, the
+// unbounded one 4.01 -> 4.15): a region's waves cannot help the region that
+// ends last.  Off by default (IPT_REGIONS = 1); the environment variable of
+// that name (a power of two <= 8) turns them on for A/B timing.
+#ifndef IPT_REGIONS
+#define IPT_REGIONS 1
+#endif
+template <int MODE>
+static int region_count(const TraceArgs &a, int grid) {
+  if (!(MODE == MODE_ADJ || MODE == MODE_ADJU || MODE == MODE_GRAPH) || a.nscenes > 1 || a.fused) return 1;
+  int R = IPT_REGIONS;
+  if (const char *e = std::getenv("IPT_REGIONS")) R = std::max(1, std::min(8, std::atoi(e)));
+  const uint64_t rows = a.W > 0 ? a.npix / (uint64_t)a.W : 0;
+  while (R > 1 && ((uint64_t)R > rows || grid % R != 0 || (R & (R - 1)) != 0)) R >>= 1;
+  return R;
 }
 
 // Chunks of a launch exactly as the kernel enumerates them (chunk_range):
@@ -1958,10 +2037,12 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
   b.chunk = 0;
   b.chunk_ctr = nullptr;
   b.chunk_base = 0;
+  b.nreg = 1;
   StreamScratch cap_ctr;  // only for a launch captured into a graph
+  GpuScene::Counters cap_cnt{st, 0, nullptr, {}};
   std::unique_lock<std::mutex> ctr_lock;  // released after the launch is enqueued
-  GpuScene::Counters *ctr = nullptr;     // advanced by `grabs` once the launch is enqueued
-  uint64_t grabs = 0;
+  GpuScene::Counters *ctr = nullptr;     // advanced by grabs[] once the launch is enqueued
+  uint64_t grabs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (IPT_DYN_CHUNKS) {
     // ~IPT_DYN_CHUNKS_PER_WAVE chunks per wave, a multiple of 64 items, 64..4096
     const uint64_t waves = (uint64_t)(a.nscenes > 1 ? b.bps : grid) * (kBlock / 64);
@@ -1979,16 +2060,35 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
     }
     // guided sizes: the last ~guided_tail() small chunks per wave end the launch
     // (non-guided instances: one size, chunk_small = chunk and no big-chunk count)
-    const uint64_t tail = BVH ? waves * (uint64_t)guided_tail() * small : 0;
-    const uint64_t nb = BVH ? (units > tail ? (units - tail) / c : 0) : 0;
     if (!BVH) small = c;
     b.chunk = (uint32_t)c;
     b.chunk_small = (uint32_t)small;
-    b.chunk_big_n = (uint32_t)nb;
-    const uint64_t chunks = launch_chunks(BVH, units, c, small, nb);
-    grabs = (chunks > waves ? chunks - waves : 0) + waves;  // per set, see TraceArgs::chunk_base
+    // per XCD region (one region = the whole launch): its units, big chunks
+    // and grabs (each of its waves grabs until one grab fails: TraceArgs::chunk_base)
+    const int R = region_count<MODE>(a, grid);
+    const uint64_t rw = waves / (uint64_t)R, rows = a.npix / (uint64_t)a.W;
+    for (int r = 0; r < R; ++r) {
+      uint64_t ur = units;
+      if (R > 1) {
+        const uint64_t rr = (rows - (uint64_t)r + (uint64_t)R - 1) / (uint64_t)R, np = rr * (uint64_t)a.W;
+        ur = np * (uint64_t)a.spp;
+        b.reg_row0[r] = a.row0 + r * a.row_step;
+        b.reg_npix[r] = np;
+        b.reg_m_npix[r] = np > 1 ? ~0ull / np + 1 : 0;
+      }
+      const uint64_t tail = BVH ? rw * (uint64_t)guided_tail() * small : 0;
+      const uint64_t nb = BVH ? (ur > tail ? (ur - tail) / c : 0) : 0;
+      b.reg_nb[r] = (uint32_t)nb;
+      if (r == 0) b.chunk_big_n = (uint32_t)nb;
+      const uint64_t chunks = launch_chunks(BVH, ur, c, small, nb);
+      grabs[r] = (chunks > rw ? chunks - rw : 0) + rw;
+    }
+    b.nreg = R;
     cap_ctr.st = st;
-    if (stream_counters(s, st, a.nscenes, &b.chunk_ctr, &b.chunk_base, &cap_ctr.p, &ctr, &ctr_lock)) return -1;
+    if (stream_counters(s, st, a.nscenes > 1 ? a.nscenes : 8, &b.chunk_ctr, &cap_ctr.p, &ctr, &cap_cnt, &ctr_lock))
+      return -1;
+    b.chunk_base = ctr->base[0];  // (a scene batch: every set's counter moves alike)
+    for (int r = 0; r < R; ++r) b.reg_base[r] = ctr->base[(size_t)r];
   }
   StreamScratch grec;  // ADJU: the vertex-record ring (TraceArgs::grec), freed behind the launch
   if (MODE == MODE_ADJU) {
@@ -2001,7 +2101,14 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
                      s->mat, kd_dev ? kd_dev : s->kd, s->emit_tri, s->emit_cdf, s->emit_pmf, out, adj, grad, target,
                      edges);
   HIP_TRY(hipGetLastError());
-  if (ctr) ctr->base += (uint32_t)grabs;  // (mod 2^32: the kernel subtracts in uint32)
+  if (ctr) {  // (mod 2^32: the kernel subtracts in uint32)
+    if (b.nreg > 1)  // region r's word
+      for (int r = 0; r < b.nreg; ++r) ctr->base[(size_t)r] += (uint32_t)grabs[r];
+    else if (a.nscenes > 1)  // every set's word
+      for (uint32_t &w : ctr->base) w += (uint32_t)grabs[0];
+    else
+      ctr->base[0] += (uint32_t)grabs[0];
+  }
   return 0;
 }
 
@@ -2149,11 +2256,21 @@ int gpu_pixel_mean_sm(const float *samples_dev, int64_t npix, int spp, float *hd
 struct FusedShape {
   int slots, group;
 };
-static FusedShape fused_shape(const RenderParams &p) {
+// BVH scenes keep the two-kernel render unless IPT_FUSED_BVH=1 (environment,
+// A/B timing): their LDS already holds the tree stage, and slots beyond
+// IPT_FUSED_BVH_WAVE_BYTES per wave cost residency.
+static FusedShape fused_shape(const RenderParams &p, bool bvh) {
   const FusedShape none = {0, 0};
   if (!IPT_FUSED_MEAN || !IPT_DYN_CHUNKS || std::getenv("IPT_RENDER_TWO_KERNEL")) return none;
   if ((uint64_t)p.width * (uint64_t)p.height * (uint64_t)p.spp > 0xffffffffull || p.spp > 256) return none;
-  const int slots = std::min(16, IPT_FUSED_WAVE_BYTES / (12 * p.spp));
+  int bytes = IPT_FUSED_WAVE_BYTES;
+  if (bvh) {
+    const char *on = std::getenv("IPT_FUSED_BVH");
+    if (!on || std::atoi(on) == 0) return none;
+    const char *b = std::getenv("IPT_FUSED_BVH_WAVE_BYTES");
+    bytes = b ? std::max(0, std::atoi(b)) : 3072;
+  }
+  const int slots = std::min(16, bytes / (12 * p.spp));
   const bool long_paths = p.max_bounces < 0 || p.max_bounces > 8;
   const int cap = slots / (long_paths ? 4 : 2);  // groups the ring holds at once
   if (cap < 1) return none;
@@ -2168,11 +2285,8 @@ int gpu_render(GpuScene *s, const RenderParams &p, const float *kd_dev, float *h
   if (check_params(s, p)) return -1;
   const int64_t npix = (int64_t)band_rows(p) * p.width;
   const int sets = p.nscenes > 1 ? p.nscenes : 1;
-  // BVH scenes keep the two-kernel render: their cooperative traversal wants
-  // the wave's rays spread over 64 pixels (a chunk's p <= 16 pixels put many
-  // lanes into the tree at once) and the slots cost the tree's LDS stage
-  // residency -- north-star 3.92 -> 4.60 ms fused (profiles/r03/fusedab_r03h.log)
-  const FusedShape fs = use_bvh(s) ? FusedShape{0, 0} : fused_shape(p);
+  // (BVH scenes: two-kernel render by default, see fused_shape)
+  const FusedShape fs = fused_shape(p, use_bvh(s));
   if (fs.group > 0) {
     TraceArgs a = make_args(s, p);
     a.fused = 1;

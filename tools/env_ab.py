@@ -73,9 +73,13 @@ def main():
         grad = torch.zeros((sc.nT, 3), dtype=torch.float64, device="cuda")
         for share in (1, 8):
             p = N.make_params(W, H, spp, mb, 0, 0, H, share)
+            pu = N.make_params(W, H, spp, None, 0, 0, H, share)  # the reference's own estimator (no bounce cap)
             calls = {"fwd": lambda: N.check(L.ipt_render_dev(sc.handle, C.byref(p), None, hdr.data_ptr(), None, st)),
                      "adj": lambda: N.check(L.ipt_adjoint_dev(sc.handle, C.byref(p), None, adj.data_ptr(),
-                                                              grad.data_ptr(), st))}
+                                                              grad.data_ptr(), st)),
+                     "fwdu": lambda: N.check(L.ipt_render_dev(sc.handle, C.byref(pu), None, hdr.data_ptr(), None, st)),
+                     "adju": lambda: N.check(L.ipt_adjoint_dev(sc.handle, C.byref(pu), None, adj.data_ptr(),
+                                                               grad.data_ptr(), st))}
             legs = args.legs.split(",")
             ref = {}
             for mname, env in modes:  # correctness against the first mode
@@ -84,10 +88,11 @@ def main():
                         grad.zero_()
                         calls[leg]()
                         torch.cuda.synchronize()
-                        v = hdr.cpu().numpy().view(np.uint32).copy() if leg == "fwd" else grad.cpu().numpy().copy()
+                        fwd = leg.startswith("fwd")
+                        v = hdr.cpu().numpy().view(np.uint32).copy() if fwd else grad.cpu().numpy().copy()
                         if leg not in ref:
                             ref[leg] = v
-                        elif leg == "fwd":
+                        elif fwd:
                             print(name, share, mname, "image bitwise:", bool(np.array_equal(v, ref[leg])), flush=True)
                         else:
                             err = float(np.max(np.abs(v - ref[leg])) / max(np.max(np.abs(ref[leg])), 1e-300))
