@@ -452,7 +452,11 @@ def main():
         for key, objs, w, h, spp, mb, desc in (
                 ("c3", SCENE0, W, H, SPP, BOUNCES, "C3: scenes/0.txt (Cornell + cube, 30 triangles), 512x512, 64 spp, 4 bounces"),
                 ("c3_unbounded", SCENE0, W, H, SPP, None, "C3 with the reference's own estimator (no bounce cap: "
-                 "Russian roulette only), scenes/0.txt, 512x512, 64 spp; adjoint = LDS ring + chunk replay"),
+                 "Russian roulette only), scenes/0.txt, 512x512, 64 spp; fused render (slot ring); adjoint = global "
+                 "record ring + chunk replay"),
+                ("legacy_create_image", SCENE0, 500, 500, 100, None, "the reference's createImage configuration "
+                 "(path_trace.cu:200-234, scene.h:8-10): scenes/0.txt, 500x500, 100 spp, no bounce cap; fused render "
+                 "(no per-sample buffer)"),
                 ("c3_northstar", NORTHSTAR, W, H, SPP, BOUNCES, "C3 as the north_star names it: Cornell + cube + "
                  "sphere.obj (assets/northstar.txt, 1310 triangles, BVH), 512x512, 64 spp, 4 bounces"),
                 ("bvh_sphere", SPHERE, W, H, SPP, BOUNCES, "Cornell + sphere.obj (1298 triangles, BVH), 512x512, 64 spp, 4 bounces"),

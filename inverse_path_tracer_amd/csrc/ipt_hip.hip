@@ -82,10 +82,10 @@ constexpr int kBlock = 256;
 constexpr int kRecSD = 3;  // specd, then speci
 constexpr int kRecFieldsDiffuse = 3;
 constexpr int kRecFieldsSpec = kRecFieldsDiffuse + 2;
-// ADJU (records in global memory): the three words of the prefix throughput
-// M_k follow, so the sweep reads M_kk instead of refolding it from the
-// chunk's first record (O(K) per path, not O(K^2))
-#define kRecMU (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse)
+// ADJU replay targets (the lane's rhi): the vertex count to replay to, and
+// two flags -- the replayed chunk ends the path (its escape terms apply) and
+// the path escaped (a miss ended it)
+constexpr int kRhiEnd = 1 << 30, kRhiEsc = 1 << 29, kRhiMask = kRhiEsc - 1;
 constexpr int kMaxAdjTris = 65535;  // tri and et share one 32-bit field
 constexpr int kEdgeW = 8;      // graph bin: w, w*f, pix[3]*w*f, light[3]*w*f
 // LDS form of the graph bins: 5 doubles per (dst, src) (w, w*f, pix[3]*w*f)
@@ -97,19 +97,29 @@ __host__ __device__ inline size_t graph_lds_doubles(int nT, int nE) {
   return (size_t)(nT + 1) * nT * kEdgeL + (size_t)(nT + 1) * (nE > 0 ? nE : 0) * 3;
 }
 constexpr int kMaxAdjBounces = 62;
-// ADJU ring slots per lane, in global memory (TraceArgs::grec: 6 words --
-// tri | et, emitter factor, coeff, and the prefix throughput M_k -- x 64
-// slots x the grid's lanes: 503 MB at C3 for 327 680 resident lanes,
-// stream-ordered scratch; a lane's live records are its current path's, so
-// the touched lines are a few slots per lane).  Smaller rings cost replays:
-// 16 slots +5% / +10% / +6% and 8 slots +13% / +27% / +23% on Cornell /
-// scenes/0 / north-star (profiles/r04/variants_trishade_ring_occ_chunk_r04c.log).  Paths of more than 64
+// ADJU ring slots per lane (3 words each, like ADJ's records: tri | et,
+// emitter factor, coeff; the prefix throughputs are rebuilt by the sweep's
+// chain from the chunk's first one, Mlo).  Round 3 kept 64 six-word slots
+// (with the recorded M_k) per lane in global memory (503 MB at C3 for 327 680
+// resident lanes): the records of the live paths overflowed the XCDs' L2s --
+// 7.5 GB fetched and 6.7 GB written per C3 launch, 48% L2 hits
+// (profiles/r04/unbounded_pmc_r04g.txt) -- and the unbounded adjoint took 1.7x
+// the unbounded forward.  Now the first IPT_ADJU_LDS_SLOTS slots of every lane
+// are in LDS (a path of up to 8 vertices never touches global memory) and the
+// ring is IPT_ADJU_RING = 24 slots, the other 16 in a global ring of 63 MB at
+// C3; a path longer than the ring replays.  Paths of more than 64
 // vertices replay their earlier chunks (a path of K vertices costs about
 // K^2 / 128 extra vertex traces).  Round 2 kept an 8-slot ring in LDS (24 KB
 // per workgroup): every path longer than 8 vertices replayed, C3 unbounded
 // adjoint 5.97 ms for a 2.73 ms forward.
 #ifndef IPT_ADJU_RING
-#define IPT_ADJU_RING 64
+#define IPT_ADJU_RING 24
+#endif
+#ifndef IPT_ADJU_LDS_SLOTS
+#define IPT_ADJU_LDS_SLOTS 8
+#endif
+#ifndef IPT_ADJU_LDS_SLOTS_BVH
+#define IPT_ADJU_LDS_SLOTS_BVH 4
 #endif
 constexpr int kAdjuRing = IPT_ADJU_RING;
 // Dynamic work distribution across the waves of a launch (TraceArgs::chunk):
@@ -196,7 +206,11 @@ struct TraceArgs {
   float rc_spp;
   float rc_W, rc_H;  // 1/W, 1/H for power-of-two sizes, else 0 (camera_ray divides)
   int rec_cap;   // ADJ: vertex records per lane (max_bounces + 1); ADJU: ring slots
-  float *grec;   // ADJU: the record ring in global memory, 3 fields x rec_cap slots x grec_stride lanes
+  // ADJU: ring slots 0 .. rec_lds-1 of every lane live in LDS ([field][slot]
+  // [lane], like ADJ's records), slots rec_lds .. rec_cap-1 in global memory
+  // (grec: fields x (rec_cap - rec_lds) slots x grec_stride lanes)
+  int rec_lds;
+  float *grec;
   uint64_t grec_stride;
   // scene batch (C5): blocks b, b + nscenes, ... (bps of them) trace material
   // set b -- interleaved, not contiguous ranges: the dispatcher fills a CU
@@ -230,8 +244,9 @@ struct TraceArgs {
   const uint32_t *pomask;
   // BVH scenes: the same masks over the large-triangle pairs (nullptr = none)
   const uint32_t *big_pomask;
-  // FWD with the pixel mean fused in (gpu_render, IPT_FUSED_MEAN): work comes
-  // in groups of `chunk` (then chunk_small) launch-local pixels x spp samples;
+  // FWD with the pixel mean fused in (gpu_render, IPT_FUSED_MEAN): a chunk of
+  // `chunk` (then chunk_small) launch-local pixels is issued in groups of
+  // `group` pixels x spp samples;
   // each pixel of a group gets one of the wave's nslots LDS slots (spp x 3
   // floats), a finished sample goes to its pixel's slot, and a slot whose
   // last sample is in is summed in sample order (toneMap) into out_samples
@@ -239,6 +254,7 @@ struct TraceArgs {
   // mean_wstride * 4 of the dynamic LDS: the slots' unfinished counts
   // [nslots], their pixels [nslots], then the slots
   int fused;
+  uint32_t group;
   uint32_t mean_off, mean_wstride;
   int nslots;
   uint8_t *ldr;
@@ -382,6 +398,9 @@ __device__ __forceinline__ void item_ray(const TraceArgs &a, uint64_t seed, uint
 #ifndef IPT_MIN_BLOCKS_ADJ
 #define IPT_MIN_BLOCKS_ADJ 5
 #endif
+#ifndef IPT_MIN_BLOCKS_ADJU
+#define IPT_MIN_BLOCKS_ADJU 5
+#endif
 #ifndef IPT_MIN_BLOCKS_GRAPH
 #define IPT_MIN_BLOCKS_GRAPH 0
 #endif
@@ -408,7 +427,9 @@ __device__ __forceinline__ void item_ray(const TraceArgs &a, uint64_t seed, uint
 template <int MODE, bool BVH>
 constexpr int min_blocks() {
   return BVH ? (is_adj<MODE>() ? IPT_MIN_BLOCKS_BVH_ADJ : (is_fwd<MODE>() ? IPT_MIN_BLOCKS_BVH_FWD : IPT_MIN_BLOCKS_BVH))
-             : (is_fwd<MODE>() ? IPT_MIN_BLOCKS_FWD : (is_adj<MODE>() ? IPT_MIN_BLOCKS_ADJ : IPT_MIN_BLOCKS_GRAPH));
+             : (is_fwd<MODE>() ? IPT_MIN_BLOCKS_FWD
+                                : (MODE == MODE_ADJU ? IPT_MIN_BLOCKS_ADJU
+                                                     : (is_adj<MODE>() ? IPT_MIN_BLOCKS_ADJ : IPT_MIN_BLOCKS_GRAPH)));
 }
 // Rejected and removed (round 3; the A/B logs under profiles/ keep the
 // evidence): a traversal-server wave per workgroup fed through an LDS ray
@@ -440,7 +461,10 @@ constexpr int min_blocks() {
 // accumulates s_memtime cycles per phase of the loop; read with
 // ipt_debug_phase_cycles (tools/phase_timing.py).
 #ifdef IPT_PHASE_TIMING
-__device__ unsigned long long g_phase_cycles[8];
+__device__ unsigned long long g_phase_cycles[10];
+// [8], [9]: the tree (coop_cast) part of phases 1 and 3 (BVH scenes)
+#define SUBPHASE_BEGIN const uint64_t ts_ = __builtin_amdgcn_s_memtime();
+#define SUBPHASE_END(i) tacc[i] += __builtin_amdgcn_s_memtime() - ts_;
 #define PHASE(i)                                     \
   {                                                  \
     const uint64_t tn_ = __builtin_amdgcn_s_memtime(); \
@@ -449,6 +473,8 @@ __device__ unsigned long long g_phase_cycles[8];
   }
 #else
 #define PHASE(i)
+#define SUBPHASE_BEGIN
+#define SUBPHASE_END(i)
 #endif
 
 // Path ray of the brute-force scenes: the unrolled pair loop with plane
@@ -672,7 +698,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   cv.stride = a.coop_stride;
   for (int k = 0; k < 6; ++k) cv.root[k] = a.root_box[k];
   if (BVH) {
-    const size_t rec_words = MODE == MODE_ADJ ? (size_t)vmax * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock : 0;  // (ADJU: global)
+    const size_t rec_words = MODE == MODE_ADJ    ? (size_t)vmax * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock
+                             : MODE == MODE_ADJU ? (size_t)a.rec_lds * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock
+                                                 : 0;
     char *base = reinterpret_cast<char *>(lds);
     const size_t off = bvh_lds_offset((size_t)(reinterpret_cast<char *>(lds_rec + rec_words) - base));
     float4 *lw = reinterpret_cast<float4 *>(base + off);
@@ -767,6 +795,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   // is held by ONE pixel, so a long path keeps one pixel's slot, not a whole
   // chunk's: the ring also serves unbounded paths.
   uint32_t glp = 0, gnp = 0, gslots = 0, fj = 0, sdone = 0;
+  uint64_t pl0 = 0, pl1 = 0;  // the grabbed chunk's pixels not yet in a group
   uint32_t sfree = MODE == MODE_FWDM ? (a.nslots >= 32 ? ~0u : (1u << a.nslots) - 1u) : 0u;
   bool started = false;
 
@@ -776,7 +805,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   V3 L = p, Le = p, Ld = p, M = mk(1.f, 1.f, 1.f);
   // ADJU (unbounded adjoint): suffix carried from the chunk after, replay
   // target (0 = first pass), next ring slot
-  V3 Scar = mk(0.f, 0.f, 0.f);
+  // and the prefix throughput at the chunk's first vertex (1 for a chunk
+  // starting at vertex 0; captured while a replay passes its start)
+  V3 Scar = mk(0.f, 0.f, 0.f), Mlo = mk(1.f, 1.f, 1.f);
   int rhi = 0, rslot = 0;
   float weight = 1.f;  // GRAPH path weight
   V3 pix = p;          // GRAPH target pixel
@@ -791,7 +822,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   // block thus runs once per vertex with most lanes on, instead of path and
   // shadow lanes serialising each other's code every iteration.
 #ifdef IPT_PHASE_TIMING
-  uint64_t tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t tacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t tp_ = __builtin_amdgcn_s_memtime();
 #endif
   const int lane = tid & 63;
@@ -860,7 +891,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     TraceArgs a = ar;
 #endif
     if (MODE == MODE_FWDM) {
-      const uint32_t G = a.chunk;  // pixels per group (the last group of a launch may hold fewer)
+      const uint32_t G = a.group;  // pixels per group (a chunk's last group may hold fewer)
       const bool issued = fj >= gnp * (uint32_t)a.spp;
       // sum the finished slots when a group's worth is waiting, when the next
       // group lacks free slots, or -- once the launch's work is handed out --
@@ -870,26 +901,29 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         sfree |= sdone;
         sdone = 0;
       }
-      // the next group of pixels (first the wave's own, then from the counter)
-      // once the current one is fully issued and G slots are free
+      // the next group of pixels (from the chunk in hand, else the wave's own
+      // chunk, then the counter's) once the current one is fully issued and
+      // G slots are free
       if (issued && !exhausted && (uint32_t)__popc(sfree) >= G) {
-        // (a wave whose own chunk is past the end grabs once, as in the
-        // unfused protocol: every wave's last grab fails, TraceArgs::chunk_base)
-        uint64_t lp0 = 0, lp1 = 0;
-        bool own = false;
-        if (!started) {
-          started = true;
-          chunk_range<BVH>(a, wave, a.npix, lp0, lp1);
-          own = lp0 < a.npix;
+        if (pl0 >= pl1) {
+          // (a wave whose own chunk is past the end grabs once, as in the
+          // unfused protocol: every wave's last grab fails, TraceArgs::chunk_base)
+          bool own = false;
+          if (!started) {
+            started = true;
+            chunk_range<BVH>(a, wave, a.npix, pl0, pl1);
+            own = pl0 < a.npix;
+          }
+          if (!own) {
+            uint32_t c = 0;
+            if (lane == 0) c = atomicAdd(a.chunk_ctr + set, 1u) - a.chunk_base;
+            chunk_range<BVH>(a, nwaves + (uint32_t)__builtin_amdgcn_readfirstlane((int)c), a.npix, pl0, pl1);  // lane 0 (full exec here)
+          }
         }
-        if (!own) {
-          uint32_t c = 0;
-          if (lane == 0) c = atomicAdd(a.chunk_ctr + set, 1u) - a.chunk_base;
-          chunk_range<BVH>(a, nwaves + (uint32_t)__builtin_amdgcn_readfirstlane((int)c), a.npix, lp0, lp1);  // lane 0 (full exec here)
-        }
-        if (lp0 < a.npix) {
-          glp = (uint32_t)lp0;
-          gnp = (uint32_t)(lp1 - lp0);
+        if (pl0 < a.npix) {
+          glp = (uint32_t)pl0;
+          gnp = (uint32_t)(pl1 - pl0 < G ? pl1 - pl0 : G);
+          pl0 += gnp;
           fj = 0;
           gslots = 0;
           uint32_t mm = sfree;
@@ -966,6 +1000,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           if (MODE == MODE_ADJU) {
             rhi = 0;
             rslot = 0;
+            Mlo = mk(1.f, 1.f, 1.f);
           }
           if (MODE == MODE_GRAPH) {
             weight = 1.f;
@@ -996,7 +1031,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         bvh_prepass<false>(bv, p, d, t, hit, -1);
         qn = coop_root_test(cv, p, d, t);
       }
+      SUBPHASE_BEGIN
       coop_cast<false>(cv, qn, p, d, t, hit);
+      SUBPHASE_END(8)
     } else if (active) {
       if (IPT_PATH_CULL && e3)
         hit = closest_hit_pairs_culled((const lds_f32 *)lds_pr, a.pboxes, nT, p, d, t);
@@ -1101,7 +1138,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         if (shadow && bvh_prepass<true>(bv, p, sd, ts, hs, et,
                                         a.big_pomask ? a.big_pomask[tri * nE + emitter] : 0xffffffffu, emitter))
           qn = coop_root_test(cv, p, sd, ts);
+        SUBPHASE_BEGIN
         coop_cast<true>(cv, qn, p, sd, ts, hs);
+        SUBPHASE_END(9)
       } else if (shadow) {
         if (IPT_SHADOW_CULL && e3)
           hs = shadow_hit_pairs_small((const lds_f32 *)lds_is, pairs, a.pboxes, e3, nT, p, sd, et, ts,
@@ -1174,20 +1213,33 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           rec[(kRecSD + 1) * fs] = speci;
         }
       }
-      if (MODE == MODE_ADJU) {  // ring slot rslot = k % rec_cap (global memory), with the prefix throughput M_k
-        gbl_f32 *rec = urec + (size_t)rslot * ustride;
-        const size_t fs = (size_t)vmax * ustride;
-        rec[0] = __uint_as_float((uint32_t)tri | ((uint32_t)emit_et << 16));
-        rec[fs] = emit_s;
-        rec[2 * fs] = coeff;
+      if (MODE == MODE_ADJU) {  // ring slot rslot = k % rec_cap: LDS or global (TraceArgs::rec_lds)
+        constexpr int NF = SPEC ? kRecFieldsSpec : kRecFieldsDiffuse;
+        float v[NF];
+        v[0] = __uint_as_float((uint32_t)tri | ((uint32_t)emit_et << 16));
+        v[1] = emit_s;
+        v[2] = coeff;
         if (SPEC) {
-          rec[kRecSD * fs] = specd;
-          rec[(kRecSD + 1) * fs] = speci;
+          v[kRecSD] = specd;
+          v[kRecSD + 1] = speci;
         }
-        rec[kRecMU * fs] = M.x;  // M before this vertex's update: the forward's own M_k
-        rec[(kRecMU + 1) * fs] = M.y;
-        rec[(kRecMU + 2) * fs] = M.z;
+        const int nl = a.rec_lds;
+        if (rslot < nl) {  // LDS slot
+          float *rec = lds_rec + (size_t)rslot * kBlock + tid;
+          const size_t fs = (size_t)nl * kBlock;
+#pragma unroll
+          for (int f = 0; f < NF; ++f) rec[f * fs] = v[f];
+        } else {  // global slot
+          gbl_f32 *rec = urec + (size_t)(rslot - nl) * ustride;
+          const size_t fs = (size_t)(vmax - nl) * ustride;
+#pragma unroll
+          for (int f = 0; f < NF; ++f) rec[f * fs] = v[f];
+        }
         rslot = (rslot + 1 == vmax) ? 0 : rslot + 1;
+        // a replay to vertex count t re-records the chunk [t - rec_cap, t): the
+        // forward's M before the update of its first vertex is the chunk's Mlo
+        const int tgt = rhi & kRhiMask;
+        if (tgt > 0 && k == (tgt > vmax ? tgt - vmax : 0)) Mlo = M;
       }
       if (MODE == MODE_GRAPH) {
         if (cont) {
@@ -1212,11 +1264,13 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       ++k;  // vertices so far
       if (cont) d = nd;
       else finished = true;
-      if (MODE == MODE_ADJU && rhi > 0 && k == rhi) finished = true;  // replay reached its chunk's end
+      if (MODE == MODE_ADJU && rhi > 0 && k == (rhi & kRhiMask)) finished = true;  // replay reached its target
     }
 
-    int uhi = 0, ulo = 0;  // ADJU: the chunk [ulo, uhi) to sweep, ufirst = the path's first pass
-    bool ufirst = false;
+    // ADJU: the chunk [ulo, uhi) to sweep; uend = it ends the path (its escape
+    // terms apply, uesc = the path escaped); urep = replay target (0: none)
+    int uhi = 0, ulo = 0, urep = 0;
+    bool uend = false, uesc = false;
     if (finished) {
       active = false;
       if (MODE == MODE_FWDM) {  // slot [channel][sample]
@@ -1230,13 +1284,28 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         o[1] = L.y;
         o[2] = L.z;
       } else if (MODE == MODE_ADJU) {
-        // the chunk [lo, hi) held by the ring -- hi = K (first pass; the
-        // escape terms of the path's end apply) or the replay target -- is
-        // swept by the wave-parallel sweep below; then, if lo > 0, the path
-        // is replayed from its camera ray to re-record [lo - rec_cap, lo)
-        ufirst = rhi == 0;
-        uhi = ufirst ? k : rhi;
-        ulo = uhi > vmax ? uhi - vmax : 0;
+        // A first pass of K <= rec_cap vertices holds the whole path: sweep
+        // [0, K) now (Mlo = 1).  A longer one replays the path from its camera
+        // ray to capture Mlo at vertex K - rec_cap (same seed, same draws, same
+        // floats; the ring then holds [K - rec_cap, K) again).  A replay that
+        // reached its target t sweeps [max(t - rec_cap, 0), t) and, if that
+        // chunk starts past vertex 0, replays again for the chunk before it.
+        const int tgt = rhi & kRhiMask;
+        if (tgt == 0) {
+          if (k <= vmax) {
+            uhi = k;
+            uend = true;
+            uesc = escaped;
+          } else {
+            urep = k | kRhiEnd | (escaped ? kRhiEsc : 0);
+          }
+        } else {
+          uhi = tgt;
+          ulo = tgt > vmax ? tgt - vmax : 0;
+          uend = (rhi & kRhiEnd) != 0;
+          uesc = (rhi & kRhiEsc) != 0;
+          if (ulo > 0) urep = ulo;
+        }
       }
     }
     if (MODE == MODE_FWDM && __ballot(finished)) {
@@ -1274,7 +1343,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       // are recorded (no left-to-right chain), the last task's suffix is the
       // chunk after's (Scar) unless this is the path's first pass, and the
       // suffix at ulo goes back to the owner for its replay.
-      const int Kf = MODE == MODE_ADJ ? ((finished && k > 0) ? k : 0) : ((finished && uhi > 0) ? uhi - ulo : 0);
+      const int Kf = MODE == MODE_ADJ ? ((finished && k > 0) ? k : 0) : (uhi > 0 ? uhi - ulo : 0);
       if (__ballot(Kf > 0)) {
         const int lane = tid & 63;
         const int inc = wave_scan_add(Kf);  // inclusive scan of the task counts over the wave
@@ -1296,7 +1365,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             wz = adj[pixel * 3 + 2] / (float)a.spp;
           }
         }
-        const size_t fs = MODE == MODE_ADJ ? (size_t)vmax * kBlock : (size_t)vmax * ustride;
+        const size_t fs = (size_t)vmax * kBlock;  // ADJ record field stride (ADJU: per slot kind, below)
         int base = 0;
         while (base < T) {  // wave-uniform
           // this round: the whole paths whose tasks end by base + 64
@@ -1311,8 +1380,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           swl[lane] = 0u;
           const int st0 = inc - Kf - base;
           const bool owns = Kf > 0 && inc <= next && st0 >= 0;
+          const bool oend = MODE == MODE_ADJ || uend, oesc = MODE == MODE_ADJ ? escaped : uesc;
           if (owns)
-            swl[st0] = (((uint32_t)st0 << 15) | (ufirst ? 1u << 14 : 0u) | (escaped ? 1u << 13 : 0u) |
+            swl[st0] = (((uint32_t)st0 << 15) | (oend ? 1u << 14 : 0u) | (oesc ? 1u << 13 : 0u) |
                         ((uint32_t)Kf << 6) | (uint32_t)lane) + 1u;
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
@@ -1323,14 +1393,15 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           const int KL = valid ? (int)((mk_ >> 6) & 127u) : 0;
           const int kk = valid ? lane - (int)(mk_ >> 15) : 0;  // task index inside the path's chunk
           const bool esc = valid && ((mk_ >> 13) & 1u);
-          const bool fst_o = MODE == MODE_ADJ || (valid && ((mk_ >> 14) & 1u));
+          const bool fst_o = MODE == MODE_ADJ || (valid && ((mk_ >> 14) & 1u));  // the chunk ends the path
           const int rr = valid ? KL - 1 - kk : 0;  // vertices after this one
           const float ax = __shfl(wx, ow), ay = __shfl(wy, ow), az = __shfl(wz, ow);
           const V3 LeL = mk(__shfl(Le.x, ow), __shfl(Le.y, ow), __shfl(Le.z, ow));
-          const V3 ML = mk(__shfl(M.x, ow), __shfl(M.y, ow), __shfl(M.z, ow));
           // this task's record (lanes past the round read vertex 0 of a valid column)
           uint32_t f0;
           float es, ck, sdv = 0.f, si = 0.f;
+          // the prefix throughput: the chunk's Mlo on its first task, passed
+          // right by the chain below (ADJ: every chunk starts at vertex 0)
           V3 Mk = mk(1.f, 1.f, 1.f);
           V3 Sc = mk(0.f, 0.f, 0.f);  // ADJU: the owner's suffix from the chunk after
           if (MODE == MODE_ADJ) {
@@ -1344,16 +1415,29 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             }
           } else {
             const int vabs = kk + __shfl(ulo, ow);  // the vertex's index on its path: ring slot vabs % rec_cap
-            const gbl_f32 *r = (const gbl_f32 *)a.grec + (size_t)blockIdx.x * kBlock + (tid & ~63) +
-                               (valid ? ow : lane) + (size_t)(vabs % vmax) * ustride;
-            f0 = valid ? __float_as_uint(r[0]) : 0u;
-            es = r[fs];
-            ck = r[2 * fs];
-            if (SPEC) {
-              sdv = r[kRecSD * fs];
-              si = r[(kRecSD + 1) * fs];
+            const int sl = vabs % vmax, nl = a.rec_lds;
+            constexpr int NF = SPEC ? kRecFieldsSpec : kRecFieldsDiffuse;
+            float rv[NF];
+            if (sl < nl) {  // LDS slot (typed: ds_read, see bins_add)
+              const lds_f32 *r = (const lds_f32 *)lds_rec + (tid & ~63) + (valid ? ow : lane) + (size_t)sl * kBlock;
+              const size_t fl = (size_t)nl * kBlock;
+#pragma unroll
+              for (int f = 0; f < NF; ++f) rv[f] = r[f * fl];
+            } else {  // global slot
+              const gbl_f32 *r = (const gbl_f32 *)a.grec + (size_t)blockIdx.x * kBlock + (tid & ~63) +
+                                 (valid ? ow : lane) + (size_t)(sl - nl) * ustride;
+              const size_t fg = (size_t)(vmax - nl) * ustride;
+#pragma unroll
+              for (int f = 0; f < NF; ++f) rv[f] = r[f * fg];
             }
-            Mk = mk(r[kRecMU * fs], r[(kRecMU + 1) * fs], r[(kRecMU + 2) * fs]);  // the forward's own M_kk
+            f0 = valid ? __float_as_uint(rv[0]) : 0u;
+            es = rv[1];
+            ck = rv[2];
+            if (SPEC) {
+              sdv = rv[kRecSD];
+              si = rv[kRecSD + 1];
+            }
+            Mk = mk(__shfl(Mlo.x, ow), __shfl(Mlo.y, ow), __shfl(Mlo.z, ow));
             Sc = mk(__shfl(Scar.x, ow), __shfl(Scar.y, ow), __shfl(Scar.z, ow));
           }
           // (the min()s keep a mis-indexed record from reaching global memory out of bounds)
@@ -1373,25 +1457,41 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           const V3 B = mk(tv.x * ck, tv.y * ck, tv.z * ck);
           V3 S = (esc && rr == 0) ? A : mk(0.f, 0.f, 0.f);
           if (MODE == MODE_ADJU && !fst_o && rr == 0) S = Sc;
-          const int kkp = MODE == MODE_ADJ ? kk : 0;  // ADJU: no prefix chain
+          const int kkp = kk;  // prefix chain: task kk takes its left neighbour's M_kk-1 T c
           // both chains in one loop (max(K) - 1 steps instead of up to twice
           // that; two independent dependency chains per step: -0.2..0.6%,
           // profiles/r03/variants_merged_r03o.log)
           const int steps = valid ? max(kkp, rr) : 0;  // this lane's chain steps
           if (__ballot(steps > 0)) {
+            // Every lane steps every round: lane i takes lane i-1's (M T) c and
+            // lane i+1's A + B S, computed here from the neighbours' operands
+            // (shifted once per round; the same float operations as in the
+            // neighbour), except a path's first task keeps its M (Mlo / 1) and
+            // its last keeps its S.  A lane's value is final after kk (M) / rr
+            // (S) steps -- its neighbour's is by then -- and stays so.  (Round 3:
+            // a select of the shifted product at step kk only; this form has no
+            // per-step compares and one shift fewer per channel.)
+            const V3 tvl = mk(wave_shr1(tv.x), wave_shr1(tv.y), wave_shr1(tv.z));
+            const float ckl = wave_shr1(ck);
+            const V3 Al = mk(wave_shl1(A.x), wave_shl1(A.y), wave_shl1(A.z));
+            const V3 Bl = mk(wave_shl1(B.x), wave_shl1(B.y), wave_shl1(B.z));
+            const bool keepM = kkp == 0, keepS = rr == 0;
             int s = 1;
             do {  // (a do-while: the loop-carried Mk, S need no copies per step)
-              const V3 N = mk((Mk.x * tv.x) * ck, (Mk.y * tv.y) * ck, (Mk.z * tv.z) * ck);
-              const V3 H = mk(A.x + B.x * S.x, A.y + B.y * S.y, A.z + B.z * S.z);
-              const V3 Nl = mk(wave_shr1(N.x), wave_shr1(N.y), wave_shr1(N.z));
-              const V3 Hr = mk(wave_shl1(H.x), wave_shl1(H.y), wave_shl1(H.z));
-              if (kkp == s) Mk = Nl;
-              if (rr == s) S = Hr;
+              const V3 Nl = mk((wave_shr1(Mk.x) * tvl.x) * ckl, (wave_shr1(Mk.y) * tvl.y) * ckl,
+                               (wave_shr1(Mk.z) * tvl.z) * ckl);
+              const V3 Hr = mk(Al.x + Bl.x * wave_shl1(S.x), Al.y + Bl.y * wave_shl1(S.y),
+                               Al.z + Bl.z * wave_shl1(S.z));
+              Mk = keepM ? Mk : Nl;
+              S = keepS ? S : Hr;
             } while (__ballot(steps > s++));
           }
           if (valid) {
             V3 dLd = Mk;
-            if (esc && rr == 0) dLd = mk(dLd.x + ML.x, dLd.y + ML.y, dLd.z + ML.z);
+            if (esc && rr == 0) {  // the escape's stale re-add weights Ld by M_K = (M_K-1 T_K-1) c_K-1
+              const V3 ML = mk((Mk.x * tv.x) * ck, (Mk.y * tv.y) * ck, (Mk.z * tv.z) * ck);
+              dLd = mk(dLd.x + ML.x, dLd.y + ML.y, dLd.z + ML.z);
+            }
             V3 gk = mk(dLd.x * lk.x, dLd.y * lk.y, dLd.z * lk.z);
             if (rr > 0 || esc || !fst_o) {
               const float cpi = div_const<2>(ck);  // ck / kPiF
@@ -1411,16 +1511,17 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           base = next;
         }
       }
-      if (MODE == MODE_ADJU && finished && ulo > 0) {  // replay the path to re-record [ulo - rec_cap, ulo)
+      if (MODE == MODE_ADJU && urep > 0) {  // replay the path from its camera ray (see the chunk choice)
         int r, c;
         item_ray(a, seed, witem, st, p, d, r, c);
         L = mk(0.f, 0.f, 0.f);
         Le = L;
         Ld = L;
         M = mk(1.f, 1.f, 1.f);
+        Mlo = M;
         k = 0;
         rslot = 0;
-        rhi = ulo;
+        rhi = urep;
         active = true;
       }
     }
@@ -1428,7 +1529,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   }
 #ifdef IPT_PHASE_TIMING
   if ((tid & 63) == 0)
-    for (int i = 0; i < 8; ++i) atomicAdd(&g_phase_cycles[i], (unsigned long long)tacc[i]);
+    for (int i = 0; i < 10; ++i) atomicAdd(&g_phase_cycles[i], (unsigned long long)tacc[i]);
 #endif
   }
 
@@ -1573,6 +1674,8 @@ struct GpuScene {
   uint32_t *pomask = nullptr;  // shadow rays' potential occluders (small scenes)
   uint32_t *big_pomask = nullptr;  // ... over the large-triangle pairs (BVH scenes)
   int accel = IPT_ACCEL_AUTO;
+  size_t adju_base = 0;  // gpu_adjoint's choice of LDS ring slots (unbounded, brute force) ...
+  int adju_nl = 0;       // ... made for this LDS base
   int *grad_map = nullptr, *slot_tri = nullptr;  // ADJ hot-set LDS slots (large scenes)
   int grid[20] = {0};       // resident workgroups per (mode, spec, bvh) (0 = not queried)
   size_t grid_lds[20] = {0};
@@ -1593,8 +1696,8 @@ struct GpuScene {
 
 #ifdef IPT_PHASE_TIMING
 extern "C" int ipt_debug_phase_cycles(unsigned long long *out) {  // read and reset
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
-  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), 10 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  unsigned long long z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof z) == hipSuccess ? 0 : -1;
 }
 #endif
@@ -1833,9 +1936,11 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
     a.cam_org[i] = std::fmaf(M[3], 1.f, std::fmaf(M[2], 0.f, std::fmaf(M[1], 0.f, M[0] * 0.f)));
   }
   a.rec_cap = p.max_bounces >= 0 ? p.max_bounces + 1 : 0;
+  a.rec_lds = 0;
   a.grec = nullptr;
   a.grec_stride = 0;
   a.chunk = 0;
+  a.group = 0;
   a.chunk_small = 0;
   a.chunk_big_n = 0;
   a.chunk_ctr = nullptr;
@@ -2055,6 +2160,7 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
       // 1/64 share 0.217 -> 0.10 ms (profiles/r03/launch_scaling_r03w.jsonl)
       c = a.chunk;
       while (c > 1 && (a.npix + c - 1) / c < waves && (c / 2) * (uint64_t)a.spp >= 64) c /= 2;
+      b.group = std::min<uint32_t>(a.group, (uint32_t)c);
       small = std::min<uint64_t>(c, std::max<uint64_t>(1, 64 / (uint64_t)a.spp));
       units = a.npix;
     }
@@ -2091,10 +2197,10 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
     for (int r = 0; r < R; ++r) b.reg_base[r] = ctr->base[(size_t)r];
   }
   StreamScratch grec;  // ADJU: the vertex-record ring (TraceArgs::grec), freed behind the launch
-  if (MODE == MODE_ADJU) {
+  if (MODE == MODE_ADJU) {  // the ring's global slots
     b.grec_stride = (uint64_t)grid * kBlock;
-    const size_t fields = (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) + 3;  // + M_k (kRecMU)
-    if (grec.alloc(fields * (size_t)a.rec_cap * b.grec_stride * sizeof(float), st)) return -1;
+    const size_t fields = SPEC ? kRecFieldsSpec : kRecFieldsDiffuse;
+    if (grec.alloc(fields * (size_t)(a.rec_cap - a.rec_lds) * b.grec_stride * sizeof(float), st)) return -1;
     b.grec = (float *)grec.p;
   }
   hipLaunchKernelGGL((trace_kernel<MODE, SPEC, BVH>), dim3(grid), dim3(kBlock), lds, st, b, s->isect, s->pairs, s->geom,
@@ -2254,13 +2360,13 @@ int gpu_pixel_mean_sm(const float *samples_dev, int64_t npix, int spp, float *hd
 #define IPT_FUSED_WAVE_BYTES 6144
 #endif
 struct FusedShape {
-  int slots, group;
+  int slots, group, per_grab;  // per_grab: groups per chunk (counter grab)
 };
 // BVH scenes keep the two-kernel render unless IPT_FUSED_BVH=1 (environment,
 // A/B timing): their LDS already holds the tree stage, and slots beyond
 // IPT_FUSED_BVH_WAVE_BYTES per wave cost residency.
 static FusedShape fused_shape(const RenderParams &p, bool bvh) {
-  const FusedShape none = {0, 0};
+  const FusedShape none = {0, 0, 0};
   if (!IPT_FUSED_MEAN || !IPT_DYN_CHUNKS || std::getenv("IPT_RENDER_TWO_KERNEL")) return none;
   if ((uint64_t)p.width * (uint64_t)p.height * (uint64_t)p.spp > 0xffffffffull || p.spp > 256) return none;
   int bytes = IPT_FUSED_WAVE_BYTES;
@@ -2277,7 +2383,11 @@ static FusedShape fused_shape(const RenderParams &p, bool bvh) {
   int g = 1;
   while (2 * g <= cap && 2 * g * p.spp <= 256) g *= 2;
   if (g * p.spp < 32) return none;  // (tiny spp: a grab per few samples; the two-kernel render wins)
-  return {slots, g};
+  // a grab hands out >= 256 samples (small groups -- spp > 128, or long
+  // paths -- would otherwise grab per pixel: the legacy 100-spp createImage
+  // issued 250 000 counter atomics, 8 MB of memory-side writes per frame)
+  const int per_grab = std::min(8, (256 + g * p.spp - 1) / (g * p.spp));
+  return {slots, g, per_grab};
 }
 
 int gpu_render(GpuScene *s, const RenderParams &p, const float *kd_dev, float *hdr_dev, uint8_t *ldr_dev,
@@ -2290,7 +2400,8 @@ int gpu_render(GpuScene *s, const RenderParams &p, const float *kd_dev, float *h
   if (fs.group > 0) {
     TraceArgs a = make_args(s, p);
     a.fused = 1;
-    a.chunk = (uint32_t)fs.group;  // pixels per group; launch_inst may halve it for thin launches
+    a.group = (uint32_t)fs.group;
+    a.chunk = (uint32_t)(fs.group * fs.per_grab);  // pixels per grab; launch_inst may halve it for thin launches
     a.nslots = fs.slots;
     a.mean_wstride = (uint32_t)(((2 * fs.slots + 3) & ~3) + 3 * fs.slots * p.spp + 3) & ~3u;  // floats per wave
     a.ldr = ldr_dev;
@@ -2326,12 +2437,45 @@ int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const f
   } else {
     a.grad_slots = s->host.nT;
   }
-  if (unbounded) a.rec_cap = kAdjuRing;
-  const size_t lds = (size_t)a.grad_slots * 3 * sizeof(double) + table_bytes(a) +
-                     (size_t)kBlock * sizeof(uint32_t) +  // the sweep's owner markers
-                     (!unbounded ? (size_t)a.rec_cap * (s->has_ks ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock *
-                                       sizeof(float)
-                                 : 0);  // (ADJU: the record ring is in global memory, launch_inst)
+  const size_t fields = (size_t)(s->has_ks ? kRecFieldsSpec : kRecFieldsDiffuse);
+  const size_t base = (size_t)a.grad_slots * 3 * sizeof(double) + table_bytes(a) +
+                      (size_t)kBlock * sizeof(uint32_t);  // + the sweep's owner markers
+  if (unbounded) {
+    // ring slots in LDS: up to IPT_ADJU_LDS_SLOTS (brute force) or
+    // IPT_ADJU_LDS_SLOTS_BVH, as many as cost no resident workgroup (the
+    // environment variable IPT_ADJU_LDS_SLOTS fixes the count, A/B timing);
+    // the rest of the ring in global memory
+    a.rec_cap = kAdjuRing;
+    const bool bvh = use_bvh(s);
+    int nl = bvh ? IPT_ADJU_LDS_SLOTS_BVH : IPT_ADJU_LDS_SLOTS;
+    const char *e = std::getenv("IPT_ADJU_LDS_SLOTS");
+    if (e) {
+      nl = std::atoi(e);
+    } else if (!bvh) {
+      const size_t per = fields * kBlock * sizeof(float);
+      if (s->adju_base != base) {  // cached per scene for this LDS base
+        int occ0 = 0;
+        HIP_TRY(s->has_ks ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, trace_kernel<MODE_ADJU, true, false>,
+                                                                         kBlock, base)
+                          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, trace_kernel<MODE_ADJU, false, false>,
+                                                                         kBlock, base));
+        int best = 0;
+        for (int k = nl; k > 0 && best == 0; --k) {
+          int o = 0;
+          HIP_TRY(s->has_ks ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, trace_kernel<MODE_ADJU, true, false>,
+                                                                           kBlock, base + k * per)
+                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, trace_kernel<MODE_ADJU, false, false>,
+                                                                           kBlock, base + k * per));
+          if (o >= occ0) best = k;
+        }
+        s->adju_base = base;
+        s->adju_nl = best;
+      }
+      nl = s->adju_nl;
+    }
+    a.rec_lds = std::max(0, std::min(nl, kAdjuRing));
+  }
+  const size_t lds = base + (size_t)(unbounded ? a.rec_lds : a.rec_cap) * fields * kBlock * sizeof(float);
   if (lds > 160 * 1024) {
     gpu_set_error("adjoint LDS footprint exceeds 160 KiB; lower max_bounces");
     return -1;

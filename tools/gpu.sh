@@ -15,6 +15,7 @@
 #   sq           SQ counter passes of the C2 headline
 #   attr         memory-side request classes of the C2 headline (atomics vs reads vs writes, TCC/TCP)
 #   valumix      VALU instruction-mix counter passes of the C2 headline
+#   uprof        kernel stats + FETCH/WRITE/TCC passes of the unbounded legs (tools/unbounded_prof.py)
 #   nsprof       rocprofv3 --kernel-trace --stats of the north-star scene (BVH instances)
 #   nspmc        FETCH/WRITE + SQ counter passes of the north-star scene
 #   scenes       tools/bench_scenes.py ($SCENES, default all)
@@ -61,6 +62,7 @@ MIX_SETS="SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_I
 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_MFMA_F32 SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM"
 BENCHQ=(python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-secondary)
 NS=(python3 "$R/tools/bench_scenes.py" --scenes northstar --brute-max-tris 0)
+UP=(python3 "$R/tools/unbounded_prof.py")
 
 run() {
   case "$1" in
@@ -74,6 +76,9 @@ run() {
     pmc) SETS=$'FETCH_SIZE\nWRITE_SIZE' pmc_passes pmc "${BENCHQ[@]}" ;;
     sq) SETS=$SQ_SETS pmc_passes sq "${BENCHQ[@]}" ;;
     attr) SETS=$ATTR_SETS pmc_passes attr "${BENCHQ[@]}" ;;
+    uprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/uprof_$T" -o run --output-format csv \
+               -- "${UP[@]}" > "$OUT/uprof_$T.log" 2>&1 &&
+           SETS=$'FETCH_SIZE\nWRITE_SIZE\nTCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum' pmc_passes upmc "${UP[@]}" --steps 2 ;;
     valumix) SETS=$MIX_SETS pmc_passes valumix "${BENCHQ[@]}" ;;
     nsprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/nsprof_$T" -o run --output-format csv \
                 -- "${NS[@]}" --steps 10 > "$OUT/nsprof_$T.log" 2>&1 ;;

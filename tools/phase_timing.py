@@ -1,7 +1,8 @@
 """Per-phase cycle breakdown of trace_kernel from the IPT_PHASE_TIMING build
 (lib/variants/libipt_phase.so): s_memtime deltas summed over waves.
 Phases: 0 refill, 1 path cast, 2 shade+draws, 3 shadow cast, 4 emitter eval,
-5 finalise (+ adjoint sweep).  Also loop iterations and mean active lanes."""
+5 finalise (+ adjoint sweep); tree_path / tree_shadow: the coop_cast part of
+phases 1 and 3 (BVH scenes).  Also loop iterations and mean active lanes."""
 import ctypes as C
 import json
 import os
@@ -31,22 +32,26 @@ def run(lib):
     for sname, recs in VB.SCENES.items():
         h = VB.scene(L, recs)
         p = N.make_params(512, 512, 64, 4, 0)
-        buf = torch.empty((512 * 512 * 64, 3), device=dev)
+        pu = N.make_params(512, 512, 64, None, 0)
+        hdr = torch.empty((512 * 512, 3), device=dev)
         adj = torch.ones((512, 512, 3), device=dev)
         g = torch.zeros((8192, 3), dtype=torch.float64, device=dev)
-        cyc = (C.c_ulonglong * 8)()
-        for kind in ("fwd", "adj"):
+        cyc = (C.c_ulonglong * 10)()
+        for kind in ("fwd", "adj", "fwdu", "adju"):  # the render (fused mean for brute-force scenes), the adjoint
             for rep in range(2):
                 L.ipt_debug_phase_cycles(cyc)
-                if kind == "fwd":
-                    assert L.ipt_render_samples_sm_dev(h, C.byref(p), None, buf.data_ptr(), st) == 0
+                q = pu if kind.endswith("u") else p
+                if kind.startswith("fwd"):
+                    assert L.ipt_render_dev(h, C.byref(q), None, hdr.data_ptr(), None, st) == 0
                 else:
-                    assert L.ipt_adjoint_dev(h, C.byref(p), None, adj.data_ptr(), g.data_ptr(), st) == 0
+                    assert L.ipt_adjoint_dev(h, C.byref(q), None, adj.data_ptr(), g.data_ptr(), st) == 0
                 torch.cuda.synchronize()
                 L.ipt_debug_phase_cycles(cyc)
             v = list(cyc)
             tot = sum(v[:6])
             res = {n: round(v[i] / tot, 4) for i, n in enumerate(NAMES)}
+            res["tree_path"] = round(v[8] / tot, 4)
+            res["tree_shadow"] = round(v[9] / tot, 4)
             res["iterations_per_wave_total"] = v[6]
             res["mean_active_lanes"] = round(v[7] / max(1, v[6]), 2)
             res["cycles_total"] = tot
