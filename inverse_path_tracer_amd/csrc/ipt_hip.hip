@@ -1471,20 +1471,43 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             // (S) steps -- its neighbour's is by then -- and stays so.  (Round 3:
             // a select of the shifted product at step kk only; this form has no
             // per-step compares and one shift fewer per channel.)
-            const V3 tvl = mk(wave_shr1(tv.x), wave_shr1(tv.y), wave_shr1(tv.z));
-            const float ckl = wave_shr1(ck);
-            const V3 Al = mk(wave_shl1(A.x), wave_shl1(A.y), wave_shl1(A.z));
-            const V3 Bl = mk(wave_shl1(B.x), wave_shl1(B.y), wave_shl1(B.z));
-            const bool keepM = kkp == 0, keepS = rr == 0;
+            float mx = Mk.x, my = Mk.y, mz = Mk.z, sx = S.x, sy = S.y, sz = S.z;
             int s = 1;
-            do {  // (a do-while: the loop-carried Mk, S need no copies per step)
-              const V3 Nl = mk((wave_shr1(Mk.x) * tvl.x) * ckl, (wave_shr1(Mk.y) * tvl.y) * ckl,
-                               (wave_shr1(Mk.z) * tvl.z) * ckl);
-              const V3 Hr = mk(Al.x + Bl.x * wave_shl1(S.x), Al.y + Bl.y * wave_shl1(S.y),
-                               Al.z + Bl.z * wave_shl1(S.z));
-              Mk = keepM ? Mk : Nl;
-              S = keepS ? S : Hr;
-            } while (__ballot(steps > s++));
+            if (MODE == MODE_ADJ) {
+              const V3 tvl = mk(wave_shr1(tv.x), wave_shr1(tv.y), wave_shr1(tv.z));
+              const float ckl = wave_shr1(ck);
+              const V3 Al = mk(wave_shl1(A.x), wave_shl1(A.y), wave_shl1(A.z));
+              const V3 Bl = mk(wave_shl1(B.x), wave_shl1(B.y), wave_shl1(B.z));
+              const bool keepM = kkp == 0, keepS = rr == 0;
+              do {  // (a do-while: the loop-carried values need no copies per step)
+                const float nx = (wave_shr1(mx) * tvl.x) * ckl, ny = (wave_shr1(my) * tvl.y) * ckl,
+                            nz = (wave_shr1(mz) * tvl.z) * ckl;
+                const float hx = Al.x + Bl.x * wave_shl1(sx), hy = Al.y + Bl.y * wave_shl1(sy),
+                            hz = Al.z + Bl.z * wave_shl1(sz);
+                mx = keepM ? mx : nx;
+                my = keepM ? my : ny;
+                mz = keepM ? mz : nz;
+                sx = keepS ? sx : hx;
+                sy = keepS ? sy : hy;
+                sz = keepS ? sz : hz;
+              } while (__ballot(steps > s++));
+            } else {  // ADJU (register pressure: no pre-shifted operands; a lane takes its neighbour's value at step kk / rr)
+              do {
+                const float nx = wave_shr1((mx * tv.x) * ck), ny = wave_shr1((my * tv.y) * ck),
+                            nz = wave_shr1((mz * tv.z) * ck);
+                const float hx = wave_shl1(A.x + B.x * sx), hy = wave_shl1(A.y + B.y * sy),
+                            hz = wave_shl1(A.z + B.z * sz);
+                const bool tm = kkp == s, ts = rr == s;
+                mx = tm ? nx : mx;
+                my = tm ? ny : my;
+                mz = tm ? nz : mz;
+                sx = ts ? hx : sx;
+                sy = ts ? hy : sy;
+                sz = ts ? hz : sz;
+              } while (__ballot(steps > s++));
+            }
+            Mk = mk(mx, my, mz);
+            S = mk(sx, sy, sz);
           }
           if (valid) {
             V3 dLd = Mk;

@@ -1,0 +1,52 @@
+"""Scratch budgets of the shipping kernel instances, read from the gfx950 code
+object's metadata in the built library (no GPU).  A scratch access in the
+trace loop costs a memory round trip per use; a refactor that makes the
+compiler put a value on the stack (e.g. a select between two whole V3
+structs, lowered to a pointer select into stack copies) shows up here before
+it shows up as a slower kernel.
+
+The diffuse brute-force instances (the C2 headline's forward, the fused
+render, the adjoint, createGraph) and the BVH adjoints carry no scratch; the
+unbounded adjoint has a few spilled VGPRs; the SPEC instances (Phong paths,
+compiled only for scenes with Ks != 0) and the BVH forwards at 5 waves/SIMD
+spill by design (ipt_hip.hip, IPT_MIN_BLOCKS_*)."""
+import os
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import code_object_resources as COR  # noqa: E402
+
+LIB = os.path.join(ROOT, "inverse_path_tracer_amd", "lib", "libipt_amd.so")
+
+# (MODE, SPEC, BVH) -> max scratch bytes per lane
+BUDGET = {
+    (0, False, False): 0,   # forward (sample buffer)
+    (4, False, False): 0,   # fused render: the C2 headline
+    (1, False, False): 0,   # adjoint: the C2 headline's gradient
+    (2, False, False): 0,   # createGraph
+    (2, False, True): 0,
+    (1, False, True): 0,    # BVH adjoint (2 waves/SIMD, 256 VGPRs allowed)
+    (3, False, True): 0,
+    (3, False, False): 16,  # unbounded adjoint: 3 spilled VGPRs
+    (0, False, True): 64,   # BVH forward at 5 waves/SIMD (spill outside the casts)
+}
+
+
+def name(mode, spec, bvh):
+    return "ipt::trace_kernel<%d, %s, %s>" % (mode, "true" if spec else "false", "true" if bvh else "false")
+
+
+@pytest.mark.skipif(not os.path.exists(COR.READELF), reason="llvm-readelf absent")
+def test_trace_kernel_scratch_budgets():
+    assert os.path.exists(LIB), "run __graft_entry__.build()"
+    r = COR.resources(LIB)
+    for key, cap in BUDGET.items():
+        k = name(*key)
+        assert k in r, k
+        assert r[k]["scratch_bytes_per_lane"] <= cap, (k, r[k])
+    # every trace_kernel instance is in the object (20 = 5 modes x SPEC x BVH)
+    assert sum(1 for k in r if k.startswith("ipt::trace_kernel<")) == 20
