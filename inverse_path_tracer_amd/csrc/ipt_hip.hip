@@ -1395,7 +1395,6 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           const bool esc = valid && ((mk_ >> 13) & 1u);
           const bool fst_o = MODE == MODE_ADJ || (valid && ((mk_ >> 14) & 1u));  // the chunk ends the path
           const int rr = valid ? KL - 1 - kk : 0;  // vertices after this one
-          const float ax = __shfl(wx, ow), ay = __shfl(wy, ow), az = __shfl(wz, ow);
           const V3 LeL = mk(__shfl(Le.x, ow), __shfl(Le.y, ow), __shfl(Le.z, ow));
           // this task's record (lanes past the round read vertex 0 of a valid column)
           uint32_t f0;
@@ -1509,6 +1508,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             Mk = mk(mx, my, mz);
             S = mk(sx, sy, sz);
           }
+          // (the owner's adjoint weights are taken only here: their global
+          // loads, issued as the sweep starts, finish under the chain)
+          const float ax = __shfl(wx, ow), ay = __shfl(wy, ow), az = __shfl(wz, ow);
           if (valid) {
             V3 dLd = Mk;
             if (esc && rr == 0) {  // the escape's stale re-add weights Ld by M_K = (M_K-1 T_K-1) c_K-1
