@@ -82,10 +82,6 @@ constexpr int kBlock = 256;
 constexpr int kRecSD = 3;  // specd, then speci
 constexpr int kRecFieldsDiffuse = 3;
 constexpr int kRecFieldsSpec = kRecFieldsDiffuse + 2;
-// ADJU replay targets (the lane's rhi): the vertex count to replay to, and
-// two flags -- the replayed chunk ends the path (its escape terms apply) and
-// the path escaped (a miss ended it)
-constexpr int kRhiEnd = 1 << 30, kRhiEsc = 1 << 29, kRhiMask = kRhiEsc - 1;
 constexpr int kMaxAdjTris = 65535;  // tri and et share one 32-bit field
 constexpr int kEdgeW = 8;      // graph bin: w, w*f, pix[3]*w*f, light[3]*w*f
 // LDS form of the graph bins: 5 doubles per (dst, src) (w, w*f, pix[3]*w*f)
@@ -107,9 +103,12 @@ constexpr int kMaxAdjBounces = 62;
 // the unbounded forward.  Now the first IPT_ADJU_LDS_SLOTS slots of every lane
 // are in LDS (a path of up to 8 vertices never touches global memory) and the
 // ring is IPT_ADJU_RING = 24 slots, the other 16 in a global ring of 63 MB at
-// C3; a path longer than the ring replays.  Paths of more than 64
-// vertices replay their earlier chunks (a path of K vertices costs about
-// K^2 / 128 extra vertex traces).  Round 2 kept an 8-slot ring in LDS (24 KB
+// C3.  Chunks are aligned to the ring: a path of K vertices is swept in chunks
+// [j R, min((j+1) R, K)), R = ring slots, the last one straight after the
+// first pass (its prefix throughput captured there at vertex j R), every
+// earlier one after a replay from the camera ray to its end (K = 30, R = 24:
+// 24 replayed vertex traces; a path of K costs about K^2 / 2R, DESIGN.md
+// §10.3).  Round 2 kept an 8-slot ring in LDS (24 KB
 // per workgroup): every path longer than 8 vertices replayed, C3 unbounded
 // adjoint 5.97 ms for a 2.73 ms forward.
 #ifndef IPT_ADJU_RING
@@ -1235,11 +1234,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
 #pragma unroll
           for (int f = 0; f < NF; ++f) rec[f * fs] = v[f];
         }
+        // a chunk starts at ring slot 0 (vertex j * rec_cap): the forward's M
+        // before the update of its first vertex is the chunk's Mlo
+        if (rslot == 0) Mlo = M;
         rslot = (rslot + 1 == vmax) ? 0 : rslot + 1;
-        // a replay to vertex count t re-records the chunk [t - rec_cap, t): the
-        // forward's M before the update of its first vertex is the chunk's Mlo
-        const int tgt = rhi & kRhiMask;
-        if (tgt > 0 && k == (tgt > vmax ? tgt - vmax : 0)) Mlo = M;
       }
       if (MODE == MODE_GRAPH) {
         if (cont) {
@@ -1264,7 +1262,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       ++k;  // vertices so far
       if (cont) d = nd;
       else finished = true;
-      if (MODE == MODE_ADJU && rhi > 0 && k == (rhi & kRhiMask)) finished = true;  // replay reached its target
+      if (MODE == MODE_ADJU && rhi > 0 && k == rhi) finished = true;  // replay reached its target
     }
 
     // ADJU: the chunk [ulo, uhi) to sweep; uend = it ends the path (its escape
@@ -1284,28 +1282,22 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         o[1] = L.y;
         o[2] = L.z;
       } else if (MODE == MODE_ADJU) {
-        // A first pass of K <= rec_cap vertices holds the whole path: sweep
-        // [0, K) now (Mlo = 1).  A longer one replays the path from its camera
-        // ray to capture Mlo at vertex K - rec_cap (same seed, same draws, same
-        // floats; the ring then holds [K - rec_cap, K) again).  A replay that
-        // reached its target t sweeps [max(t - rec_cap, 0), t) and, if that
-        // chunk starts past vertex 0, replays again for the chunk before it.
-        const int tgt = rhi & kRhiMask;
-        if (tgt == 0) {
-          if (k <= vmax) {
-            uhi = k;
-            uend = true;
-            uesc = escaped;
-          } else {
-            urep = k | kRhiEnd | (escaped ? kRhiEsc : 0);
-          }
+        // The first pass sweeps the path's last chunk [b, K), b = the last
+        // multiple of rec_cap below K (its records are the ring's slots 0 ..
+        // K - b - 1, its Mlo was captured at vertex b).  A replay to vertex b
+        // (same seed, same draws, same floats) re-records [b - rec_cap, b) in
+        // slots 0 .. rec_cap - 1 and captures that chunk's Mlo; it is swept with
+        // the suffix carried from the chunk after (Scar), and so on to vertex 0.
+        if (rhi == 0) {
+          uhi = k;
+          ulo = k > 0 ? k - (rslot == 0 ? vmax : rslot) : 0;  // (rslot = K % rec_cap)
+          uend = true;
+          uesc = escaped;
         } else {
-          uhi = tgt;
-          ulo = tgt > vmax ? tgt - vmax : 0;
-          uend = (rhi & kRhiEnd) != 0;
-          uesc = (rhi & kRhiEsc) != 0;
-          if (ulo > 0) urep = ulo;
+          uhi = rhi;
+          ulo = rhi - vmax;
         }
+        if (ulo > 0) urep = ulo;
       }
     }
     if (MODE == MODE_FWDM && __ballot(finished)) {
@@ -1339,10 +1331,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       // recomputed both chains per task from the owner's LDS column (O(K^2)
       // record reads, loops as long as the wave's longest chain).
       // MODE_ADJU sweeps the chunk [ulo, uhi) of each finished lane the same
-      // way, from its records in global memory: there the prefix throughputs
-      // are recorded (no left-to-right chain), the last task's suffix is the
-      // chunk after's (Scar) unless this is the path's first pass, and the
-      // suffix at ulo goes back to the owner for its replay.
+      // way, from its ring slots (LDS, then global): the prefix chain starts
+      // from the chunk's captured Mlo, the last task's suffix is the chunk
+      // after's (Scar) unless the chunk ends the path, and the suffix at ulo
+      // goes back to the owner for its replay.
       const int Kf = MODE == MODE_ADJ ? ((finished && k > 0) ? k : 0) : (uhi > 0 ? uhi - ulo : 0);
       if (__ballot(Kf > 0)) {
         const int lane = tid & 63;
@@ -1413,8 +1405,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
               si = r[(kRecSD + 1) * fs];
             }
           } else {
-            const int vabs = kk + __shfl(ulo, ow);  // the vertex's index on its path: ring slot vabs % rec_cap
-            const int sl = vabs % vmax, nl = a.rec_lds;
+            const int sl = kk, nl = a.rec_lds;  // the vertex's ring slot (chunks start at slot 0)
             constexpr int NF = SPEC ? kRecFieldsSpec : kRecFieldsDiffuse;
             float rv[NF];
             if (sl < nl) {  // LDS slot (typed: ds_read, see bins_add)
