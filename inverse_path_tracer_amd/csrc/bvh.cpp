@@ -38,6 +38,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <limits>
 
 namespace ipt {
@@ -437,9 +438,55 @@ std::vector<uint32_t> shadow_occluder_masks(const HostScene &S, const std::vecto
 
 // Collapse the binary tree into 8-wide nodes: starting from a binary node's
 // two children, repeatedly open the inner child with the largest box until
-// the node has 8 children or only leaves remain.  Leaves keep their binary
-// triangle sets (<= 16 triangles), re-laid as single TriIsect records.
+// the node has 8 children or only leaves remain.  An inner binary node whose
+// subtree holds at most kWideLeafTris triangles is not opened but becomes one
+// leaf with all of them: the cooperative traversal tests a leaf's triangles
+// 8 at a time (one triangle per lane), so a leaf of 8 costs one round -- one
+// dependent load -- where the binary SAH's leaves of ~2 (its cost counts
+// pairs) cost a node level each.  Leaves are re-laid as single TriIsect
+// records (<= 16 per leaf).  IPT_WIDE_LEAF_TRIS (environment, scene load)
+// overrides the bound; 0 keeps the binary leaves.  North-star scene: 81 wide
+// nodes of depth 4 -> 73 of depth 3, 214 leaves of 6 triangles on average;
+// forward 3.843 -> 3.782 ms, adjoint 4.698 -> 4.623 (bound 16: 4.23 / 5.02,
+// the leaves' boxes grow; profiles/r04/envab_wideleaf_r04n.log).
+#ifndef IPT_WIDE_LEAF_TRIS
+#define IPT_WIDE_LEAF_TRIS 8
+#endif
 static bool build_wide(HostScene *S) {
+  const char *wl = std::getenv("IPT_WIDE_LEAF_TRIS");
+  const int fat = std::min(16, std::max(0, wl ? std::atoi(wl) : IPT_WIDE_LEAF_TRIS));
+  // triangles of a binary child code (leaf: its pairs' real triangles)
+  std::vector<int> tris_of_node(S->bvh_nodes.size(), -1);
+  std::function<int(int)> count = [&](int code) -> int {
+    if (code < 0) {
+      const int c = ~code, first = c >> kBvhLeafPairBits, np = (c & ((1 << kBvhLeafPairBits) - 1)) + 1;
+      int n = 0;
+      for (int j = first; j < first + np; ++j)
+        for (int hh = 0; hh < 2; ++hh) n += S->bvh_pairs[(size_t)j].idx[hh] != 0x7fffffff;
+      return n;
+    }
+    int &m = tris_of_node[(size_t)code];
+    if (m < 0) {
+      int kid[2];
+      std::memcpy(kid, &S->bvh_nodes[(size_t)code].q[3][0], sizeof kid);
+      m = count(kid[0]) + count(kid[1]);
+    }
+    return m;
+  };
+  std::function<void(int, std::vector<int> &)> gather = [&](int code, std::vector<int> &out) {
+    if (code < 0) {
+      const int c = ~code, first = c >> kBvhLeafPairBits, np = (c & ((1 << kBvhLeafPairBits) - 1)) + 1;
+      for (int j = first; j < first + np; ++j)
+        for (int hh = 0; hh < 2; ++hh)
+          if (S->bvh_pairs[(size_t)j].idx[hh] != 0x7fffffff) out.push_back(S->bvh_pairs[(size_t)j].idx[hh]);
+      return;
+    }
+    int kid[2];
+    std::memcpy(kid, &S->bvh_nodes[(size_t)code].q[3][0], sizeof kid);
+    gather(kid[0], out);
+    gather(kid[1], out);
+  };
+  auto openable = [&](int code) { return code >= 0 && count(code) > fat; };
   struct Child {
     float lo[3], hi[3];
     int code;  // binary child code
@@ -482,7 +529,7 @@ static bool build_wide(HostScene *S) {
     while (kids.size() < 8) {
       int best = -1;
       for (size_t k = 0; k < kids.size(); ++k)
-        if (kids[k].code >= 0 && (best < 0 || area(kids[k]) > area(kids[(size_t)best]))) best = (int)k;
+        if (openable(kids[k].code) && (best < 0 || area(kids[k]) > area(kids[(size_t)best]))) best = (int)k;
       if (best < 0) break;
       const int n = kids[(size_t)best].code;
       kids[(size_t)best] = child_of(n, 0);
@@ -499,21 +546,18 @@ static bool build_wide(HostScene *S) {
           sl[a] = c.lo[a];
           sl[3 + a] = c.hi[a];
         }
-        if (c.code >= 0) {
+        if (openable(c.code)) {
           ref = (int32_t)queue.size();  // wide node h is queue[h]: a child's index is its queue position
           queue.push_back({c.code, depth + 1});
-        } else {
-          const int code = ~c.code;
-          const int first = code >> kBvhLeafPairBits, np = (code & ((1 << kBvhLeafPairBits) - 1)) + 1;
+        } else {  // a binary leaf, or a subtree of <= fat triangles: one leaf
+          std::vector<int> ts;
+          gather(c.code, ts);
           const int tfirst = (int)S->bvh_wtris.size();
-          for (int j = first; j < first + np; ++j)
-            for (int hh = 0; hh < 2; ++hh) {
-              const int t = S->bvh_pairs[(size_t)j].idx[hh];
-              if (t == 0x7fffffff) continue;
-              TriIsect T = S->isect[(size_t)t];
-              std::memcpy(&T.pad[0], &t, sizeof t);
-              S->bvh_wtris.push_back(T);
-            }
+          for (const int t : ts) {
+            TriIsect T = S->isect[(size_t)t];
+            std::memcpy(&T.pad[0], &t, sizeof t);
+            S->bvh_wtris.push_back(T);
+          }
           const int cnt = (int)S->bvh_wtris.size() - tfirst;
           if (cnt < 1 || cnt > 16 || tfirst >= (1 << 26)) {
             S->bvh_status = "leaf too large for the cooperative traversal";

@@ -63,10 +63,18 @@ const char *gpu_last_error() { return g_gpu_err.c_str(); }
 // replaying the path from its camera ray (same seed, same draws, so the same
 // floats) -- see trace_kernel.
 // MODE_FWDM: MODE_FWD with the pixel mean fused in (gpu_render, TraceArgs::fused).
-enum { MODE_FWD = 0, MODE_ADJ = 1, MODE_GRAPH = 2, MODE_ADJU = 3, MODE_FWDM = 4 };
+// MODE_ADJW: MODE_ADJ compiled for 6 waves/SIMD instead of 5 (80 VGPRs), for
+// full-size launches (gpu_adjoint: C2 adjoint 1.914 -> 1.862 ms, scenes/0
+// 2.316 -> 2.275; a C2 1/8 share is slower with it, 0.307 -> 0.320 ms,
+// profiles/r04/variants_chain_adj6_r04l.log, envab_adjw_r04m.log); brute-force diffuse scenes only.
+enum { MODE_FWD = 0, MODE_ADJ = 1, MODE_GRAPH = 2, MODE_ADJU = 3, MODE_FWDM = 4, MODE_ADJW = 5 };
+template <int MODE>
+constexpr bool is_badj() {  // the bounded adjoint (either occupancy)
+  return MODE == MODE_ADJ || MODE == MODE_ADJW;
+}
 template <int MODE>
 constexpr bool is_adj() {
-  return MODE == MODE_ADJ || MODE == MODE_ADJU;
+  return is_badj<MODE>() || MODE == MODE_ADJU;
 }
 template <int MODE>
 constexpr bool is_fwd() {
@@ -111,6 +119,9 @@ constexpr int kMaxAdjBounces = 62;
 // §10.3).  Round 2 kept an 8-slot ring in LDS (24 KB
 // per workgroup): every path longer than 8 vertices replayed, C3 unbounded
 // adjoint 5.97 ms for a 2.73 ms forward.
+#ifndef IPT_ADJU_SHIFTED_CHAIN  // the bounded adjoint's chain form in MODE_ADJU too (A/B)
+#define IPT_ADJU_SHIFTED_CHAIN 0
+#endif
 #ifndef IPT_ADJU_RING
 #define IPT_ADJU_RING 24
 #endif
@@ -207,7 +218,7 @@ struct TraceArgs {
   int rec_cap;   // ADJ: vertex records per lane (max_bounces + 1); ADJU: ring slots
   // ADJU: ring slots 0 .. rec_lds-1 of every lane live in LDS ([field][slot]
   // [lane], like ADJ's records), slots rec_lds .. rec_cap-1 in global memory
-  // (grec: fields x (rec_cap - rec_lds) slots x grec_stride lanes)
+  // (grec: grec_stride lanes x (rec_cap - rec_lds) slots x fields)
   int rec_lds;
   float *grec;
   uint64_t grec_stride;
@@ -400,6 +411,9 @@ __device__ __forceinline__ void item_ray(const TraceArgs &a, uint64_t seed, uint
 #ifndef IPT_MIN_BLOCKS_ADJU
 #define IPT_MIN_BLOCKS_ADJU 5
 #endif
+#ifndef IPT_MIN_BLOCKS_ADJW
+#define IPT_MIN_BLOCKS_ADJW 6
+#endif
 #ifndef IPT_MIN_BLOCKS_GRAPH
 #define IPT_MIN_BLOCKS_GRAPH 0
 #endif
@@ -427,8 +441,9 @@ template <int MODE, bool BVH>
 constexpr int min_blocks() {
   return BVH ? (is_adj<MODE>() ? IPT_MIN_BLOCKS_BVH_ADJ : (is_fwd<MODE>() ? IPT_MIN_BLOCKS_BVH_FWD : IPT_MIN_BLOCKS_BVH))
              : (is_fwd<MODE>() ? IPT_MIN_BLOCKS_FWD
-                                : (MODE == MODE_ADJU ? IPT_MIN_BLOCKS_ADJU
-                                                     : (is_adj<MODE>() ? IPT_MIN_BLOCKS_ADJ : IPT_MIN_BLOCKS_GRAPH)));
+                                : (MODE == MODE_ADJU   ? IPT_MIN_BLOCKS_ADJU
+                                   : MODE == MODE_ADJW ? IPT_MIN_BLOCKS_ADJW
+                                                       : (is_adj<MODE>() ? IPT_MIN_BLOCKS_ADJ : IPT_MIN_BLOCKS_GRAPH)));
 }
 // Rejected and removed (round 3; the A/B logs under profiles/ keep the
 // evidence): a traversal-server wave per workgroup fed through an LDS ray
@@ -697,7 +712,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   cv.stride = a.coop_stride;
   for (int k = 0; k < 6; ++k) cv.root[k] = a.root_box[k];
   if (BVH) {
-    const size_t rec_words = MODE == MODE_ADJ    ? (size_t)vmax * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock
+    const size_t rec_words = is_badj<MODE>()    ? (size_t)vmax * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock
                              : MODE == MODE_ADJU ? (size_t)a.rec_lds * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock
                                                  : 0;
     char *base = reinterpret_cast<char *>(lds);
@@ -745,13 +760,17 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     }
   };
 
-  // MODE_ADJU: the vertex-record ring lives in global memory (TraceArgs::grec,
-  // [field][slot][lane of the grid]: a lane's records are ustride floats apart)
+  // MODE_ADJU: the ring's global slots (TraceArgs::grec, [lane of the grid]
+  // [slot][field]: ustride floats per lane, a record's fields contiguous -- one
+  // 12-B store per vertex, and a sweep round reads an owner's consecutive
+  // records as one contiguous run.  Round 4's first form, [field][slot][lane],
+  // stored 4 B per field at a different place per lane: three write requests
+  // per vertex, 767 MB written per C3 launch, profiles/r04/unbounded_pmc_r04l.txt)
   gbl_f32 *urec = nullptr;
   size_t ustride = 0;
   if (MODE == MODE_ADJU) {
-    ustride = a.grec_stride;
-    urec = (gbl_f32 *)a.grec + (size_t)blockIdx.x * kBlock + tid;
+    ustride = (size_t)(a.rec_cap - a.rec_lds) * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse);
+    urec = (gbl_f32 *)a.grec + ((size_t)blockIdx.x * kBlock + tid) * ustride;
   }
   {  // the wave's persistent loop
   // wave-uniform sample range (static partition, regenerated per lane)
@@ -1201,7 +1220,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     PHASE(4)
     // ================= finalise the vertex
     if (vertex) {
-      if (MODE == MODE_ADJ) {  // vertex record k (layout [field][vertex][lane])
+      if (is_badj<MODE>()) {  // vertex record k (layout [field][vertex][lane])
         float *rec = lds_rec + (size_t)k * kBlock + tid;
         const size_t fs = (size_t)vmax * kBlock;
         rec[0] = __uint_as_float((uint32_t)tri | ((uint32_t)emit_et << 16));
@@ -1229,10 +1248,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
 #pragma unroll
           for (int f = 0; f < NF; ++f) rec[f * fs] = v[f];
         } else {  // global slot
-          gbl_f32 *rec = urec + (size_t)(rslot - nl) * ustride;
-          const size_t fs = (size_t)(vmax - nl) * ustride;
+          gbl_f32 *rec = urec + (size_t)(rslot - nl) * NF;
 #pragma unroll
-          for (int f = 0; f < NF; ++f) rec[f * fs] = v[f];
+          for (int f = 0; f < NF; ++f) rec[f] = v[f];
         }
         // a chunk starts at ring slot 0 (vertex j * rec_cap): the forward's M
         // before the update of its first vertex is the chunk's Mlo
@@ -1335,7 +1353,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       // from the chunk's captured Mlo, the last task's suffix is the chunk
       // after's (Scar) unless the chunk ends the path, and the suffix at ulo
       // goes back to the owner for its replay.
-      const int Kf = MODE == MODE_ADJ ? ((finished && k > 0) ? k : 0) : (uhi > 0 ? uhi - ulo : 0);
+      const int Kf = is_badj<MODE>() ? ((finished && k > 0) ? k : 0) : (uhi > 0 ? uhi - ulo : 0);
       if (__ballot(Kf > 0)) {
         const int lane = tid & 63;
         const int inc = wave_scan_add(Kf);  // inclusive scan of the task counts over the wave
@@ -1372,7 +1390,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           swl[lane] = 0u;
           const int st0 = inc - Kf - base;
           const bool owns = Kf > 0 && inc <= next && st0 >= 0;
-          const bool oend = MODE == MODE_ADJ || uend, oesc = MODE == MODE_ADJ ? escaped : uesc;
+          const bool oend = is_badj<MODE>() || uend, oesc = is_badj<MODE>() ? escaped : uesc;
           if (owns)
             swl[st0] = (((uint32_t)st0 << 15) | (oend ? 1u << 14 : 0u) | (oesc ? 1u << 13 : 0u) |
                         ((uint32_t)Kf << 6) | (uint32_t)lane) + 1u;
@@ -1385,7 +1403,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           const int KL = valid ? (int)((mk_ >> 6) & 127u) : 0;
           const int kk = valid ? lane - (int)(mk_ >> 15) : 0;  // task index inside the path's chunk
           const bool esc = valid && ((mk_ >> 13) & 1u);
-          const bool fst_o = MODE == MODE_ADJ || (valid && ((mk_ >> 14) & 1u));  // the chunk ends the path
+          const bool fst_o = is_badj<MODE>() || (valid && ((mk_ >> 14) & 1u));  // the chunk ends the path
           const int rr = valid ? KL - 1 - kk : 0;  // vertices after this one
           const V3 LeL = mk(__shfl(Le.x, ow), __shfl(Le.y, ow), __shfl(Le.z, ow));
           // this task's record (lanes past the round read vertex 0 of a valid column)
@@ -1395,7 +1413,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           // right by the chain below (ADJ: every chunk starts at vertex 0)
           V3 Mk = mk(1.f, 1.f, 1.f);
           V3 Sc = mk(0.f, 0.f, 0.f);  // ADJU: the owner's suffix from the chunk after
-          if (MODE == MODE_ADJ) {
+          if (is_badj<MODE>()) {
             const float *r = lds_rec + (tid & ~63) + (valid ? ow : lane) + (size_t)kk * kBlock;
             f0 = valid ? __float_as_uint(r[0]) : 0u;
             es = r[fs];
@@ -1414,11 +1432,11 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
 #pragma unroll
               for (int f = 0; f < NF; ++f) rv[f] = r[f * fl];
             } else {  // global slot
-              const gbl_f32 *r = (const gbl_f32 *)a.grec + (size_t)blockIdx.x * kBlock + (tid & ~63) +
-                                 (valid ? ow : lane) + (size_t)(sl - nl) * ustride;
-              const size_t fg = (size_t)(vmax - nl) * ustride;
+              const gbl_f32 *r = (const gbl_f32 *)a.grec +
+                                 ((size_t)blockIdx.x * kBlock + (tid & ~63) + (valid ? ow : lane)) * ustride +
+                                 (size_t)(sl - nl) * NF;
 #pragma unroll
-              for (int f = 0; f < NF; ++f) rv[f] = r[f * fg];
+              for (int f = 0; f < NF; ++f) rv[f] = r[f];
             }
             f0 = valid ? __float_as_uint(rv[0]) : 0u;
             es = rv[1];
@@ -1463,7 +1481,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             // per-step compares and one shift fewer per channel.)
             float mx = Mk.x, my = Mk.y, mz = Mk.z, sx = S.x, sy = S.y, sz = S.z;
             int s = 1;
-            if (MODE == MODE_ADJ) {
+            if (is_badj<MODE>() || IPT_ADJU_SHIFTED_CHAIN) {
               const V3 tvl = mk(wave_shr1(tv.x), wave_shr1(tv.y), wave_shr1(tv.z));
               const float ckl = wave_shr1(ck);
               const V3 Al = mk(wave_shl1(A.x), wave_shl1(A.y), wave_shl1(A.z));
@@ -1693,11 +1711,12 @@ struct GpuScene {
   size_t adju_base = 0;  // gpu_adjoint's choice of LDS ring slots (unbounded, brute force) ...
   int adju_nl = 0;       // ... made for this LDS base
   int *grad_map = nullptr, *slot_tri = nullptr;  // ADJ hot-set LDS slots (large scenes)
-  int grid[20] = {0};       // resident workgroups per (mode, spec, bvh) (0 = not queried)
-  size_t grid_lds[20] = {0};
-  size_t pick_base[20] = {0};  // launch_bvh's LDS choice per (mode, spec): base bytes it was made for
-  size_t pick_tail[20] = {0};  // ... and the per-block tail (fused pixel mean slots) behind it
-  int pick_opt[20] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+  int grid[24] = {0};       // resident workgroups per (mode, spec, bvh) (0 = not queried)
+  size_t grid_lds[24] = {0};
+  size_t pick_base[24] = {0};  // launch_bvh's LDS choice per (mode, spec): base bytes it was made for
+  size_t pick_tail[24] = {0};  // ... and the per-block tail (fused pixel mean slots) behind it
+  int pick_opt[24] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1,
+                      -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
   // dynamic-chunk counters per (stream, number of sets): zeroed once, then
   // advanced by every launch by a known amount (TraceArgs::chunk_base)
   struct Counters {
@@ -2099,7 +2118,7 @@ static int stream_counters(GpuScene *s, hipStream_t st, int words, uint32_t **ou
 #endif
 template <int MODE>
 static int region_count(const TraceArgs &a, int grid) {
-  if (!(MODE == MODE_ADJ || MODE == MODE_ADJU || MODE == MODE_GRAPH) || a.nscenes > 1 || a.fused) return 1;
+  if (!(is_badj<MODE>() || MODE == MODE_ADJU || MODE == MODE_GRAPH) || a.nscenes > 1 || a.fused) return 1;
   int R = IPT_REGIONS;
   if (const char *e = std::getenv("IPT_REGIONS")) R = std::max(1, std::min(8, std::atoi(e)));
   const uint64_t rows = a.W > 0 ? a.npix / (uint64_t)a.W : 0;
@@ -2303,7 +2322,10 @@ static int launch(GpuScene *s, TraceArgs a, size_t lds, const float *kd_dev, flo
       lds = a.mean_off + tail;
     }
   };
-  if (use_bvh(s)) {
+  if constexpr (MODE == MODE_ADJW) {  // (gpu_adjoint: brute-force diffuse scenes only)
+    add_tail();
+    return launch_inst<MODE, false, false>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
+  } else if (use_bvh(s)) {
     if (s->has_ks) {
       if (launch_bvh_pick<MODE, true>(s, a, &lds, tail)) return -1;
       add_tail();
@@ -2312,10 +2334,11 @@ static int launch(GpuScene *s, TraceArgs a, size_t lds, const float *kd_dev, flo
     if (launch_bvh_pick<MODE, false>(s, a, &lds, tail)) return -1;
     add_tail();
     return launch_inst<MODE, false, true>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
+  } else {
+    add_tail();
+    if (s->has_ks) return launch_inst<MODE, true, false>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
+    return launch_inst<MODE, false, false>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
   }
-  add_tail();
-  if (s->has_ks) return launch_inst<MODE, true, false>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
-  return launch_inst<MODE, false, false>(s, a, lds, kd_dev, out, adj, grad, target, edges, st);
 }
 
 int gpu_render_samples(GpuScene *s, const RenderParams &p, const float *kd_dev, float *samples_dev, void *stream) {
@@ -2432,6 +2455,11 @@ int gpu_render(GpuScene *s, const RenderParams &p, const float *kd_dev, float *h
   return pixel_mean_sm_sets((const float *)ws.p, npix, p.spp, sets, hdr_dev, ldr_dev, stream);
 }
 
+// Bounded adjoint launches of at least this many samples (all material sets)
+// use MODE_ADJW: C2 (16.8 M) gains 2.7%, a C2 1/8 share (2.1 M) loses 4%.
+#ifndef IPT_ADJW_MIN_SAMPLES
+#define IPT_ADJW_MIN_SAMPLES (8ull << 20)
+#endif
 int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const float *adj_dev, double *grad_dev,
                 void *stream) {
   if (check_params(s, p)) return -1;
@@ -2498,6 +2526,13 @@ int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const f
   }
   if (unbounded)
     return launch<MODE_ADJU>(s, a, lds, kd_dev, nullptr, adj_dev, grad_dev, nullptr, nullptr, (hipStream_t)stream);
+  // the 6-wave instance for full-size launches whose LDS leaves room for a
+  // sixth workgroup per CU (IPT_ADJW=0/1 in the environment forces the choice)
+  bool wide = !use_bvh(s) && !s->has_ks && 6 * lds <= 160 * 1024 &&
+              (uint64_t)a.n_samples * (uint64_t)std::max(1, a.nscenes) >= IPT_ADJW_MIN_SAMPLES;
+  if (const char *e = std::getenv("IPT_ADJW")) wide = std::atoi(e) != 0 && !use_bvh(s) && !s->has_ks;
+  if (wide)
+    return launch<MODE_ADJW>(s, a, lds, kd_dev, nullptr, adj_dev, grad_dev, nullptr, nullptr, (hipStream_t)stream);
   return launch<MODE_ADJ>(s, a, lds, kd_dev, nullptr, adj_dev, grad_dev, nullptr, nullptr, (hipStream_t)stream);
 }
 

@@ -27,6 +27,7 @@ BUDGET = {
     (0, False, False): 0,   # forward (sample buffer)
     (4, False, False): 0,   # fused render: the C2 headline
     (1, False, False): 0,   # adjoint: the C2 headline's gradient
+    (5, False, False): 16,  # adjoint at 6 waves/SIMD (80 VGPRs, full-size launches): 3 spilled VGPRs
     (2, False, False): 0,   # createGraph
     (2, False, True): 0,
     (1, False, True): 0,    # BVH adjoint (2 waves/SIMD, 256 VGPRs allowed)
@@ -48,5 +49,5 @@ def test_trace_kernel_scratch_budgets():
         k = name(*key)
         assert k in r, k
         assert r[k]["scratch_bytes_per_lane"] <= cap, (k, r[k])
-    # every trace_kernel instance is in the object (20 = 5 modes x SPEC x BVH)
-    assert sum(1 for k in r if k.startswith("ipt::trace_kernel<")) == 20
+    # every trace_kernel instance is in the object (5 modes x SPEC x BVH, + the 6-wave adjoint)
+    assert sum(1 for k in r if k.startswith("ipt::trace_kernel<")) == 21

@@ -147,6 +147,18 @@ def test_adjoint_matches_oracle(scenes, name, W, H, spp, mb, seed):
     np.testing.assert_allclose(g, want, rtol=1e-9, atol=1e-12)
 
 
+@pytest.mark.parametrize("name,W,H,spp,mb,seed", [("scene0", 64, 64, 8, 4, 3), ("cornell", 48, 48, 8, 2, 6)])
+def test_adjoint_six_wave_instance_matches_oracle(scenes, monkeypatch, name, W, H, spp, mb, seed):
+    """MODE_ADJW (the bounded adjoint at 6 waves/SIMD, chosen for launches
+    of >= 8 M samples) forced onto small launches: same gradient."""
+    monkeypatch.setenv("IPT_ADJW", "1")
+    P, Q = scenes[name]
+    adj = np.random.RandomState(seed).uniform(-1, 1, (H, W, 3)).astype(np.float32)
+    g = P.adjoint(adj, W, H, spp, mb, seed)
+    want = Q.adjoint(W, H, spp, mb, seed, adj)
+    np.testing.assert_allclose(g, want, rtol=1e-9, atol=1e-12)
+
+
 def test_back_to_back_launches_with_ragged_chunks(scenes):
     """Launches on one stream share the chunk counters, each starting from the
     base the host advanced by the previous launch's grabs (ipt_hip.hip

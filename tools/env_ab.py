@@ -56,6 +56,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--scenes", default="cornell,scene0,northstar")
     ap.add_argument("--legs", default="fwd,adj")
+    ap.add_argument("--scene-env", action="store_true",
+                    help="load each mode's own copy of the scene under its environment (scene-load switches, "
+                         "e.g. IPT_WIDE_LEAF_TRIS)")
     args = ap.parse_args()
     modes = [parse_mode(m) for m in args.modes]
     torch.cuda.set_device(0)
@@ -69,20 +72,32 @@ def main():
     recs = {"cornell": CORNELL, "scene0": SCENE0, "northstar": NORTHSTAR}
     out = {}
     for name in args.scenes.split(","):
-        sc = product_scene(recs[name])
-        grad = torch.zeros((sc.nT, 3), dtype=torch.float64, device="cuda")
+        scs = {}
+        for mname, env in modes:
+            if args.scene_env or not scs:
+                with Env(env if args.scene_env else {}):
+                    scs[mname] = product_scene(recs[name])
+            else:
+                scs[mname] = next(iter(scs.values()))
+        nT = next(iter(scs.values())).nT
+        grad = torch.zeros((nT, 3), dtype=torch.float64, device="cuda")
         for share in (1, 8):
             p = N.make_params(W, H, spp, mb, 0, 0, H, share)
             pu = N.make_params(W, H, spp, None, 0, 0, H, share)  # the reference's own estimator (no bounce cap)
-            calls = {"fwd": lambda: N.check(L.ipt_render_dev(sc.handle, C.byref(p), None, hdr.data_ptr(), None, st)),
-                     "adj": lambda: N.check(L.ipt_adjoint_dev(sc.handle, C.byref(p), None, adj.data_ptr(),
-                                                              grad.data_ptr(), st)),
-                     "fwdu": lambda: N.check(L.ipt_render_dev(sc.handle, C.byref(pu), None, hdr.data_ptr(), None, st)),
-                     "adju": lambda: N.check(L.ipt_adjoint_dev(sc.handle, C.byref(pu), None, adj.data_ptr(),
-                                                               grad.data_ptr(), st))}
+
+            def mode_calls(sc):
+                return {"fwd": lambda: N.check(L.ipt_render_dev(sc.handle, C.byref(p), None, hdr.data_ptr(), None, st)),
+                        "adj": lambda: N.check(L.ipt_adjoint_dev(sc.handle, C.byref(p), None, adj.data_ptr(),
+                                                                 grad.data_ptr(), st)),
+                        "fwdu": lambda: N.check(L.ipt_render_dev(sc.handle, C.byref(pu), None, hdr.data_ptr(), None,
+                                                                 st)),
+                        "adju": lambda: N.check(L.ipt_adjoint_dev(sc.handle, C.byref(pu), None, adj.data_ptr(),
+                                                                  grad.data_ptr(), st))}
+            mcalls = {mname: mode_calls(scs[mname]) for mname, _ in modes}
             legs = args.legs.split(",")
             ref = {}
             for mname, env in modes:  # correctness against the first mode
+                calls = mcalls[mname]
                 with Env(env):
                     for leg in legs:
                         grad.zero_()
@@ -100,6 +115,7 @@ def main():
             times = {(m, leg): [] for m, _ in modes for leg in legs}
             for rnd in range(args.rounds):
                 for mname, env in modes:
+                    calls = mcalls[mname]
                     with Env(env):
                         for leg in legs:
                             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -114,7 +130,8 @@ def main():
                 key = "%s:1/%d:%s:%s" % (name, share, leg, mname)
                 out[key] = round(float(np.median(v)), 4)
                 print(key, out[key], flush=True)
-        sc.close()
+        for sc in {id(v): v for v in scs.values()}.values():
+            sc.close()
     print(json.dumps(out), flush=True)
 
 
