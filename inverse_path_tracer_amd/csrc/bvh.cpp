@@ -574,9 +574,11 @@ static bool build_wide(HostScene *S) {
       std::memcpy(&sl[6], &ref, sizeof ref);
     }
     // Front-to-back child order per ray-direction octant o (bit a set: d_a <
-    // 0), 3 bits per rank, kept in slot o's pad word: rank by the centre's
-    // coordinate sum signed by the octant, empty slots last.  Only the visit
-    // order of the octant-ordered traversal (IPT_BVH_OCTANT) depends on it.
+    // 0), kept in slot o's pad word as each child's RANK, 3 bits per child
+    // (bits 3k: the rank of child k): rank by the centre's coordinate sum
+    // signed by the octant, empty slots last.  Lane k of a traversal group
+    // reads child k and this word at once (coop_cast); only the visit order
+    // depends on it.
     for (int o = 0; o < 8; ++o) {
       int order[8];
       double key[8];
@@ -588,9 +590,9 @@ static bool build_wide(HostScene *S) {
             key[k] += ((o >> a) & 1 ? -0.5 : 0.5) * ((double)kids[(size_t)k].lo[a] + kids[(size_t)k].hi[a]);
       }
       std::stable_sort(order, order + 8, [&](int x, int y) { return key[x] < key[y]; });
-      uint32_t perm = 0;
-      for (int r = 0; r < 8; ++r) perm |= (uint32_t)order[r] << (3 * r);
-      std::memcpy(&W.s[o][7], &perm, sizeof perm);
+      uint32_t rank = 0;
+      for (int r = 0; r < 8; ++r) rank |= (uint32_t)r << (3 * order[r]);
+      std::memcpy(&W.s[o][7], &rank, sizeof rank);
     }
     S->bvh_wide.push_back(W);
   }

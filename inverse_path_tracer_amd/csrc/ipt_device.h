@@ -932,12 +932,17 @@ __device__ __forceinline__ bool bvh_prepass(const BvhView &B, V3 p, V3 d, float 
 // branch is group-uniform and the DPP reductions (xor 1, xor 2 within quads,
 // half-row mirror) only read lanes of the same, active group.
 constexpr int kWideF4 = 16;  // float4 per wide node (WideNode, 256 B)
-// Lane j of a group tests the child of rank j in the ray octant's
-// precomputed front-to-back order (bvh.cpp, slot o's pad word), so the next
-// node is the lowest set bit of the hit mask -- no DPP distance reduction per
-// visit (~15 VALU), one extra dependent LDS read.  Exact either way (the
-// visit order never changes the lexicographic result); sphere scene forward
-// 7.04 -> 6.69 ms, north-star 8.90 -> 8.57 ms (profiles/r02_variants_octant.log).
+#ifndef IPT_COOP_SPLIT
+#define IPT_COOP_SPLIT 0
+#endif
+// Children are visited in the ray octant's precomputed front-to-back order
+// (bvh.cpp: slot o's pad word holds each child's rank): lane j reads child j
+// and that word with independent LDS reads, the group ORs 1 << rank(j) of its
+// hit children (three DPP stages) and the next node is the hit child of the
+// lowest rank, broadcast by a DPP min -- one LDS round trip per visit.  (Round
+// 2's form read the word first, then child perm[j], and broadcast the next
+// node with ds_bpermute: three dependent LDS round trips.)  Exact either way:
+// the visit order never changes the lexicographic result.
 struct CoopView {
   const float4 *wn;    // wide nodes (WideNode, kWideF4 float4 each)
   bool wn_lds;         // wn points into LDS (else global memory)
@@ -965,6 +970,12 @@ __device__ __forceinline__ int min_dpp(int v) {
   return min(v, __builtin_amdgcn_update_dpp(0x7fffffff, v, CTRL, 0xf, 0xf, false));
 }
 __device__ __forceinline__ int group_min_i32(int v) { return min_dpp<0x141>(min_dpp<0x4E>(min_dpp<0xB1>(v))); }
+template <int CTRL>
+__device__ __forceinline__ uint32_t or_dpp(uint32_t v) {
+  return v | (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+}
+// OR over the 8 lanes of each group (same three stages as group_min_i32)
+__device__ __forceinline__ uint32_t group_or_u32(uint32_t v) { return or_dpp<0x141>(or_dpp<0x4E>(or_dpp<0xB1>(v))); }
 // Lexicographic minimum of (t, i) over the 8 lanes of each group.  Every t
 // here is an accepted hit parameter (>= kEpsUp) or +inf, never NaN or
 // negative, so its bit pattern orders like its value: the minimum t is an
@@ -1049,28 +1060,46 @@ __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3
 #ifdef IPT_BVH_STATS
       uint32_t st_nodes = 0, st_leaves = 0;
 #endif
+#if IPT_COOP_SPLIT
+      // Each step first ISSUES its memory reads -- node groups their node
+      // (LDS), leaf groups their first 8 triangles (global) -- and only then
+      // computes, so when some groups of the wave are at nodes and others at
+      // leaves the two latencies overlap instead of adding up (the node and
+      // leaf code run one after the other under SIMT).
       for (;;) {
-        if (node >= 0) {  // wide node: lane j tests child j
+        v4f qa = {0.f, 0.f, 0.f, 0.f}, qb = qa, t0 = qa, t1 = qa, t2 = qa, t3 = qa, t4 = qa;
+        uint32_t rw = 0;
+        if (node >= 0) {
+          if (C.wn_lds) {
+            rw = __float_as_uint(((const lds_f32 *)C.wn)[4 * (2 * (8 * node + oct) + 1) + 3]);
+            const lds_v4 *q = (const lds_v4 *)C.wn + 2 * (8 * node + j);
+            qa = q[0];
+            qb = q[1];
+          } else {
+            rw = __float_as_uint(((const gbl_f32 *)C.wn)[4 * (2 * (8 * node + oct) + 1) + 3]);
+            const gbl_v4 *q = (const gbl_v4 *)C.wn + 2 * (8 * node + j);
+            qa = q[0];
+            qb = q[1];
+          }
+        } else {
+          const int code = ~node;
+          if (j <= (code & 15)) {
+            const gbl_v4 *tp = (const gbl_v4 *)(C.wt + (code >> 4) + j);
+            t0 = tp[0];
+            t1 = tp[1];
+            t2 = tp[2];
+            t3 = tp[3];
+            t4 = tp[4];
+          }
+        }
+        int nd = node;
+        asm volatile("" : "+v"(nd));  // (keeps the compiler from re-merging the two halves per branch)
+        if (nd >= 0) {  // wide node: lane j tests child j (rank rj in the octant order)
 #ifdef IPT_BVH_STATS
           ++st_nodes;
 #endif
-          // lane j tests the child of rank j in the ray octant's front-to-back order
-          float4 a, b;
-          if (C.wn_lds) {  // typed per branch: ds_read_b128, not a flat load
-            const lds_f32 *pw = (const lds_f32 *)C.wn + 4 * (2 * (8 * node + oct) + 1) + 3;
-            const uint32_t sj = (__float_as_uint(*pw) >> (3 * j)) & 7u;
-            const lds_v4 *q = (const lds_v4 *)C.wn + 2 * (8 * node + (int)sj);
-            const v4f qa = q[0], qb = q[1];
-            a = make_float4(qa.x, qa.y, qa.z, qa.w);
-            b = make_float4(qb.x, qb.y, qb.z, qb.w);
-          } else {
-            const gbl_f32 *pw = (const gbl_f32 *)C.wn + 4 * (2 * (8 * node + oct) + 1) + 3;
-            const uint32_t sj = (__float_as_uint(*pw) >> (3 * j)) & 7u;
-            const gbl_v4 *q = (const gbl_v4 *)C.wn + 2 * (8 * node + (int)sj);
-            const v4f qa = q[0], qb = q[1];
-            a = make_float4(qa.x, qa.y, qa.z, qa.w);
-            b = make_float4(qb.x, qb.y, qb.z, qb.w);
-          }
+          const uint32_t rj = (rw >> (3 * j)) & 7u;
+          const float4 a = make_float4(qa.x, qa.y, qa.z, qa.w), b = make_float4(qb.x, qb.y, qb.z, qb.w);
           const int ref = __float_as_int(b.z);
           const float tx0 = fmaf(a.x, r.ix.x, r.ox.x), tx1 = fmaf(a.w, r.ix.x, r.ox.x);
           const float ty0 = fmaf(a.y, r.iy.x, r.oy.x), ty1 = fmaf(b.x, r.iy.x, r.oy.x);
@@ -1078,16 +1107,92 @@ __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3
           const float en = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.f));
           const float ex = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), gt));
           const bool h = en <= ex && ref != kWideEmpty;
-          const uint32_t hm = (uint32_t)(__ballot(h) >> (lane & 56)) & 0xffu;
+          const uint32_t hm = group_or_u32(h ? 1u << rj : 0u);
+          if (hm == 0) {
+            node = sp > 0 ? (int)stk[--sp] : kBvhDone;
+          } else {
+            const uint32_t f = (uint32_t)__builtin_ctz(hm);
+            const int nx = group_min_i32(h && rj == f ? ref : 0x7fffffff);
+            const uint32_t others = hm & (hm - 1u);
+            if ((others >> rj) & 1u) stk[sp + __popc(others >> (rj + 1))] = (uint32_t)ref;
+            sp += __popc(others);
+            node = nx;
+          }
+        } else {  // leaf: lane j tests triangle j, 8 per round (the first 8 read above)
+#ifdef IPT_BVH_STATS
+          ++st_leaves;
+#endif
+          const int code = ~nd;
+          const int first = code >> 4, cnt = (code & 15) + 1;
+#ifdef IPT_BVH_STATS
+          if (j == 0) atomicAdd(&g_bvh_stats[4], (unsigned long long)cnt);
+#endif
+          for (int base = 0; base < cnt; base += 8) {
+            float tj = __builtin_inff();
+            int ij = 0x7fffffff;
+            if (base + j < cnt) {
+              TriIsect T;
+              if (base == 0) {
+                const float v[20] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w, t2.x, t2.y,
+                                     t2.z, t2.w, t3.x, t3.y, t3.z, t3.w, t4.x, t4.y, t4.z, t4.w};
+                __builtin_memcpy(&T, v, sizeof T);
+              } else {
+                T = C.wt[first + base + j];
+              }
+              tj = tri_accept_t(T, gp, gd);
+              ij = __float_as_int(T.pad[0]);
+            }
+            group_lexmin(tj, ij);
+            const bool take = (tj < gt) | ((tj == gt) & (ij < gi));
+            gt = take ? tj : gt;
+            gi = take ? ij : gi;
+          }
+          node = (SHADOW && gi != target) ? kBvhDone : (sp > 0 ? (int)stk[--sp] : kBvhDone);
+        }
+        if (node == kBvhDone) break;
+      }
+#else
+      for (;;) {
+        if (node >= 0) {  // wide node: lane j tests child j
+#ifdef IPT_BVH_STATS
+          ++st_nodes;
+#endif
+          // lane j tests child j; its rank in the ray octant's front-to-back order
+          float4 a, b;
+          uint32_t rw;
+          if (C.wn_lds) {  // typed per branch: ds_read_b128, not a flat load
+            const lds_f32 *pw = (const lds_f32 *)C.wn + 4 * (2 * (8 * node + oct) + 1) + 3;
+            const lds_v4 *q = (const lds_v4 *)C.wn + 2 * (8 * node + j);
+            rw = __float_as_uint(*pw);
+            const v4f qa = q[0], qb = q[1];
+            a = make_float4(qa.x, qa.y, qa.z, qa.w);
+            b = make_float4(qb.x, qb.y, qb.z, qb.w);
+          } else {
+            const gbl_f32 *pw = (const gbl_f32 *)C.wn + 4 * (2 * (8 * node + oct) + 1) + 3;
+            const gbl_v4 *q = (const gbl_v4 *)C.wn + 2 * (8 * node + j);
+            rw = __float_as_uint(*pw);
+            const v4f qa = q[0], qb = q[1];
+            a = make_float4(qa.x, qa.y, qa.z, qa.w);
+            b = make_float4(qb.x, qb.y, qb.z, qb.w);
+          }
+          const uint32_t rj = (rw >> (3 * j)) & 7u;
+          const int ref = __float_as_int(b.z);
+          const float tx0 = fmaf(a.x, r.ix.x, r.ox.x), tx1 = fmaf(a.w, r.ix.x, r.ox.x);
+          const float ty0 = fmaf(a.y, r.iy.x, r.oy.x), ty1 = fmaf(b.x, r.iy.x, r.oy.x);
+          const float tz0 = fmaf(a.z, r.iz.x, r.oz.x), tz1 = fmaf(b.y, r.iz.x, r.oz.x);
+          const float en = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.f));
+          const float ex = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), gt));
+          const bool h = en <= ex && ref != kWideEmpty;
+          const uint32_t hm = group_or_u32(h ? 1u << rj : 0u);  // hit children by rank
           if (hm == 0) {
             node = sp > 0 ? (int)stk[--sp] : kBvhDone;
           } else {
             // next = the nearest-ranked hit child; the other hits are pushed
             // farthest first, so they pop in front-to-back order
-            const int f = __builtin_ctz(hm);
-            const int nx = __builtin_amdgcn_ds_bpermute(((lane & 56) + f) << 2, ref);
+            const uint32_t f = (uint32_t)__builtin_ctz(hm);
+            const int nx = group_min_i32(h && rj == f ? ref : 0x7fffffff);
             const uint32_t others = hm & (hm - 1u);
-            if ((others >> j) & 1u) stk[sp + __popc(others >> (j + 1))] = (uint32_t)ref;
+            if ((others >> rj) & 1u) stk[sp + __popc(others >> (rj + 1))] = (uint32_t)ref;
             sp += __popc(others);
             node = nx;
           }
@@ -1117,6 +1222,7 @@ __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3
         }
         if (node == kBvhDone) break;
       }
+#endif
 #ifdef IPT_BVH_STATS
       if (j == 0) {
         atomicAdd(&g_bvh_stats[0], 1ull);

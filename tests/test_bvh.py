@@ -273,8 +273,8 @@ def test_never_hit_triangle_left_out(tmp_path):
 def test_wide_nodes_nest_and_order_children(name):
     """WideNode (scene_layout.h, bvh.cpp build_wide): every inner child's own
     children lie inside the box its parent slot stores, and each slot's pad
-    word is a permutation of the 8 children (the octant front-to-back order
-    the cooperative traversal's lane j reads)."""
+    word gives the 8 children's ranks in the octant front-to-back order (a
+    permutation; the cooperative traversal's lane j reads child j's rank)."""
     from conftest import NORTHSTAR
 
     recs = {"sphere": SPHERE_SCENE, "clutter": CLUTTER_SCENE, "northstar": NORTHSTAR}[name]
