@@ -932,9 +932,6 @@ __device__ __forceinline__ bool bvh_prepass(const BvhView &B, V3 p, V3 d, float 
 // branch is group-uniform and the DPP reductions (xor 1, xor 2 within quads,
 // half-row mirror) only read lanes of the same, active group.
 constexpr int kWideF4 = 16;  // float4 per wide node (WideNode, 256 B)
-#ifndef IPT_COOP_SPLIT
-#define IPT_COOP_SPLIT 0
-#endif
 // Children are visited in the ray octant's precomputed front-to-back order
 // (bvh.cpp: slot o's pad word holds each child's rank): lane j reads child j
 // and that word with independent LDS reads, the group ORs 1 << rank(j) of its
@@ -942,7 +939,11 @@ constexpr int kWideF4 = 16;  // float4 per wide node (WideNode, 256 B)
 // lowest rank, broadcast by a DPP min -- one LDS round trip per visit.  (Round
 // 2's form read the word first, then child perm[j], and broadcast the next
 // node with ds_bpermute: three dependent LDS round trips.)  Exact either way:
-// the visit order never changes the lexicographic result.
+// the visit order never changes the lexicographic result.  (Rejected: a step
+// that first issued every group's reads -- node from LDS, or the leaf's
+// triangles -- and then computed, so node and leaf latencies would overlap:
+// north-star forward 3.78 -> 4.92 ms, adjoint 4.55 -> 7.53, the triangle
+// registers held across the step spilled; profiles/r04/variants_coop_split_r04p.log.)
 struct CoopView {
   const float4 *wn;    // wide nodes (WideNode, kWideF4 float4 each)
   bool wn_lds;         // wn points into LDS (else global memory)
@@ -1060,98 +1061,6 @@ __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3
 #ifdef IPT_BVH_STATS
       uint32_t st_nodes = 0, st_leaves = 0;
 #endif
-#if IPT_COOP_SPLIT
-      // Each step first ISSUES its memory reads -- node groups their node
-      // (LDS), leaf groups their first 8 triangles (global) -- and only then
-      // computes, so when some groups of the wave are at nodes and others at
-      // leaves the two latencies overlap instead of adding up (the node and
-      // leaf code run one after the other under SIMT).
-      for (;;) {
-        v4f qa = {0.f, 0.f, 0.f, 0.f}, qb = qa, t0 = qa, t1 = qa, t2 = qa, t3 = qa, t4 = qa;
-        uint32_t rw = 0;
-        if (node >= 0) {
-          if (C.wn_lds) {
-            rw = __float_as_uint(((const lds_f32 *)C.wn)[4 * (2 * (8 * node + oct) + 1) + 3]);
-            const lds_v4 *q = (const lds_v4 *)C.wn + 2 * (8 * node + j);
-            qa = q[0];
-            qb = q[1];
-          } else {
-            rw = __float_as_uint(((const gbl_f32 *)C.wn)[4 * (2 * (8 * node + oct) + 1) + 3]);
-            const gbl_v4 *q = (const gbl_v4 *)C.wn + 2 * (8 * node + j);
-            qa = q[0];
-            qb = q[1];
-          }
-        } else {
-          const int code = ~node;
-          if (j <= (code & 15)) {
-            const gbl_v4 *tp = (const gbl_v4 *)(C.wt + (code >> 4) + j);
-            t0 = tp[0];
-            t1 = tp[1];
-            t2 = tp[2];
-            t3 = tp[3];
-            t4 = tp[4];
-          }
-        }
-        int nd = node;
-        asm volatile("" : "+v"(nd));  // (keeps the compiler from re-merging the two halves per branch)
-        if (nd >= 0) {  // wide node: lane j tests child j (rank rj in the octant order)
-#ifdef IPT_BVH_STATS
-          ++st_nodes;
-#endif
-          const uint32_t rj = (rw >> (3 * j)) & 7u;
-          const float4 a = make_float4(qa.x, qa.y, qa.z, qa.w), b = make_float4(qb.x, qb.y, qb.z, qb.w);
-          const int ref = __float_as_int(b.z);
-          const float tx0 = fmaf(a.x, r.ix.x, r.ox.x), tx1 = fmaf(a.w, r.ix.x, r.ox.x);
-          const float ty0 = fmaf(a.y, r.iy.x, r.oy.x), ty1 = fmaf(b.x, r.iy.x, r.oy.x);
-          const float tz0 = fmaf(a.z, r.iz.x, r.oz.x), tz1 = fmaf(b.y, r.iz.x, r.oz.x);
-          const float en = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.f));
-          const float ex = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), gt));
-          const bool h = en <= ex && ref != kWideEmpty;
-          const uint32_t hm = group_or_u32(h ? 1u << rj : 0u);
-          if (hm == 0) {
-            node = sp > 0 ? (int)stk[--sp] : kBvhDone;
-          } else {
-            const uint32_t f = (uint32_t)__builtin_ctz(hm);
-            const int nx = group_min_i32(h && rj == f ? ref : 0x7fffffff);
-            const uint32_t others = hm & (hm - 1u);
-            if ((others >> rj) & 1u) stk[sp + __popc(others >> (rj + 1))] = (uint32_t)ref;
-            sp += __popc(others);
-            node = nx;
-          }
-        } else {  // leaf: lane j tests triangle j, 8 per round (the first 8 read above)
-#ifdef IPT_BVH_STATS
-          ++st_leaves;
-#endif
-          const int code = ~nd;
-          const int first = code >> 4, cnt = (code & 15) + 1;
-#ifdef IPT_BVH_STATS
-          if (j == 0) atomicAdd(&g_bvh_stats[4], (unsigned long long)cnt);
-#endif
-          for (int base = 0; base < cnt; base += 8) {
-            float tj = __builtin_inff();
-            int ij = 0x7fffffff;
-            if (base + j < cnt) {
-              TriIsect T;
-              if (base == 0) {
-                const float v[20] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w, t2.x, t2.y,
-                                     t2.z, t2.w, t3.x, t3.y, t3.z, t3.w, t4.x, t4.y, t4.z, t4.w};
-                __builtin_memcpy(&T, v, sizeof T);
-              } else {
-                T = C.wt[first + base + j];
-              }
-              tj = tri_accept_t(T, gp, gd);
-              ij = __float_as_int(T.pad[0]);
-            }
-            group_lexmin(tj, ij);
-            const bool take = (tj < gt) | ((tj == gt) & (ij < gi));
-            gt = take ? tj : gt;
-            gi = take ? ij : gi;
-          }
-          node = (SHADOW && gi != target) ? kBvhDone : (sp > 0 ? (int)stk[--sp] : kBvhDone);
-        }
-        if (node == kBvhDone) break;
-      }
-#else
       for (;;) {
         if (node >= 0) {  // wide node: lane j tests child j
 #ifdef IPT_BVH_STATS
@@ -1222,7 +1131,6 @@ __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3
         }
         if (node == kBvhDone) break;
       }
-#endif
 #ifdef IPT_BVH_STATS
       if (j == 0) {
         atomicAdd(&g_bvh_stats[0], 1ull);
