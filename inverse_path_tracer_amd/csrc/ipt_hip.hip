@@ -110,8 +110,11 @@ constexpr int kMaxAdjBounces = 62;
 // (profiles/r04/unbounded_pmc_r04g.txt) -- and the unbounded adjoint took 1.7x
 // the unbounded forward.  Now the first IPT_ADJU_LDS_SLOTS slots of every lane
 // are in LDS (a path of up to 8 vertices never touches global memory) and the
-// ring is IPT_ADJU_RING = 24 slots, the other 16 in a global ring of 63 MB at
-// C3.  Chunks are aligned to the ring: a path of K vertices is swept in chunks
+// rest of the ring is global: as many slots as IPT_ADJU_RING_MB (64 MB) holds
+// for the launch's resident lanes, up to IPT_ADJU_RING slots in all -- 24 at
+// C3 (8 + 16, 327 680 lanes), 31 for the north-star BVH instance (4 + 27,
+// fewer resident lanes; 32 vs 24 slots there: 8.67 -> 8.34 ms,
+// profiles/r04/variants_adju_ushift_ring_r04m.log).  Chunks are aligned to the ring: a path of K vertices is swept in chunks
 // [j R, min((j+1) R, K)), R = ring slots, the last one straight after the
 // first pass (its prefix throughput captured there at vertex j R), every
 // earlier one after a replay from the camera ray to its end (K = 30, R = 24:
@@ -123,7 +126,10 @@ constexpr int kMaxAdjBounces = 62;
 #define IPT_ADJU_SHIFTED_CHAIN 0
 #endif
 #ifndef IPT_ADJU_RING
-#define IPT_ADJU_RING 24
+#define IPT_ADJU_RING 32
+#endif
+#ifndef IPT_ADJU_RING_MB
+#define IPT_ADJU_RING_MB 64
 #endif
 #ifndef IPT_ADJU_LDS_SLOTS
 #define IPT_ADJU_LDS_SLOTS 8
@@ -2235,7 +2241,11 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
   if (MODE == MODE_ADJU) {  // the ring's global slots
     b.grec_stride = (uint64_t)grid * kBlock;
     const size_t fields = SPEC ? kRecFieldsSpec : kRecFieldsDiffuse;
-    if (grec.alloc(fields * (size_t)(a.rec_cap - a.rec_lds) * b.grec_stride * sizeof(float), st)) return -1;
+    // the ring: the LDS slots, then as many global ones as the budget holds
+    const size_t per_slot = fields * (size_t)b.grec_stride * sizeof(float);
+    const size_t fit = ((size_t)IPT_ADJU_RING_MB << 20) / per_slot;
+    b.rec_cap = a.rec_lds + (int)std::max<size_t>(1, std::min<size_t>(fit, (size_t)(kAdjuRing - a.rec_lds)));
+    if (grec.alloc(fields * (size_t)(b.rec_cap - b.rec_lds) * b.grec_stride * sizeof(float), st)) return -1;
     b.grec = (float *)grec.p;
   }
   hipLaunchKernelGGL((trace_kernel<MODE, SPEC, BVH>), dim3(grid), dim3(kBlock), lds, st, b, s->isect, s->pairs, s->geom,
@@ -2517,7 +2527,7 @@ int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const f
       }
       nl = s->adju_nl;
     }
-    a.rec_lds = std::max(0, std::min(nl, kAdjuRing));
+    a.rec_lds = std::max(0, std::min(nl, kAdjuRing - 1));  // (launch_inst sizes the global part)
   }
   const size_t lds = base + (size_t)(unbounded ? a.rec_lds : a.rec_cap) * fields * kBlock * sizeof(float);
   if (lds > 160 * 1024) {
