@@ -420,6 +420,16 @@ def main():
     t_wall = time.perf_counter()
     fwd_ms = cx.timed(lambda i: head.fwd(i, piped=True), args.steps, head.streams)
     wall_fwd = time.perf_counter() - t_wall
+    # the last two frames in flight, re-rendered alone: bitwise the same images
+    last = list(range(max(0, args.steps - 2), args.steps))
+    got = {i: head.hdr2[i % 2].clone() for i in last}  # (hdr2[0] is head.hdr, which fwd(i) overwrites)
+    piped_ok = []
+    for i in last:
+        head.fwd(i)
+        torch.cuda.synchronize()
+        piped_ok.append(bool(torch.equal(got[i].view(torch.int32), head.hdr.view(torch.int32))))
+    if not all(piped_ok):
+        print("bench: frames in flight differ from frames rendered alone: %s" % piped_ok, file=sys.stderr)
     # (gloo, the one-GPU rehearsal backend, stages every all-reduce through the
     # host: there the adjoint steps stay on one stream)
     piped_adj = world == 1 or backend == "nccl"
@@ -432,7 +442,8 @@ def main():
                         "grad_value": round(args.steps * frame / (bwd_serial_ms / 1e3) / 1e6, 2),
                         "ms_per_step": round(fwd_serial_ms / args.steps, 4),
                         "grad_ms_per_step": round(bwd_serial_ms / args.steps, 4),
-                        "workload": "the headline's frames one after another on ONE stream (no frame overlap)"}}
+                        "workload": "the headline's frames one after another on ONE stream (no frame overlap)"},
+             "piped_frames_bitwise_equal_alone": piped_ok}
     if not args.no_secondary:
         # sustained rates (>= 0.5 s of back-to-back steps per leg; DVFS-steady)
         k, ms = cx.sustained(lambda i: head.fwd(i))

@@ -2102,7 +2102,13 @@ static int stream_counters(GpuScene *s, hipStream_t st, int words, uint32_t **ou
   if (!c) {
     uint32_t *dev = nullptr;
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(&dev), (size_t)words * sizeof(uint32_t)));
-    HIP_TRY(hipMemset(dev, 0, (size_t)words * sizeof(uint32_t)));
+    // zeroed ON the launch stream: a blocking hipMemset goes to the null
+    // stream, which a non-blocking stream (every torch stream) does not wait
+    // for -- behind queued null-stream work the zeroing landed after this
+    // stream's first launch had advanced the counter, every later launch's
+    // base was off and its waves ran dry early (frames in flight rendered
+    // only part of the image; caught by bench.py's bitwise check)
+    HIP_TRY(hipMemsetAsync(dev, 0, (size_t)words * sizeof(uint32_t), st));
     s->counters.push_back({st, words, dev, std::vector<uint32_t>((size_t)words, 0u)});
     c = &s->counters.back();
   }

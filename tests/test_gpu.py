@@ -184,6 +184,52 @@ def test_back_to_back_launches_with_ragged_chunks(scenes):
     assert np.array_equal(bits(hdr.reshape(-1, 3)), bits(hq))
 
 
+def test_new_stream_behind_busy_null_stream():
+    """A stream's chunk counters are created (and zeroed) at its first
+    launch.  Zeroed with a blocking hipMemset they were ordered on the null
+    stream, which a non-blocking torch stream does not wait for: behind queued
+    null-stream work the zeroing landed after the new stream's first launch
+    had advanced the counter, and every later launch on that stream rendered
+    part of its frame (bench.py's frames in flight).  Now zeroed on the launch
+    stream: launches on a fresh stream behind a busy null stream are bitwise
+    the null stream's."""
+    import torch
+
+    from inverse_path_tracer_amd import _native as N
+
+    L = N.lib()
+    hip = C.CDLL("libamdhip64.so")
+    sc = product_scene(CORNELL)
+    try:
+        W = H = 256
+        ps = [N.make_params(W, H, 64, 4, 5 + i) for i in range(3)]
+        null = torch.cuda.current_stream()
+        ref = [torch.empty((W * H, 3), device="cuda") for _ in ps]
+        for p, r in zip(ps, ref):
+            N.check(L.ipt_render_dev(sc.handle, C.byref(p), None, r.data_ptr(), None, null.cuda_stream))
+        torch.cuda.synchronize()
+        for trial in range(3):
+            busy = torch.empty((W * H, 3), device="cuda")
+            for _ in range(6):  # queued null-stream work
+                N.check(L.ipt_render_dev(sc.handle, C.byref(ps[0]), None, busy.data_ptr(), None, null.cuda_stream))
+            # a raw non-blocking stream never used before (torch's stream pool
+            # may hand back one whose counters already exist)
+            raw = C.c_void_p()
+            assert hip.hipStreamCreateWithFlags(C.byref(raw), 1) == 0  # hipStreamNonBlocking
+            st = torch.cuda.ExternalStream(raw.value)
+            got = [torch.full((W * H, 3), float("nan"), device="cuda") for _ in ps]
+            torch.cuda.synchronize()
+            for _ in range(6):
+                N.check(L.ipt_render_dev(sc.handle, C.byref(ps[0]), None, busy.data_ptr(), None, null.cuda_stream))
+            for p, g in zip(ps, got):
+                N.check(L.ipt_render_dev(sc.handle, C.byref(p), None, g.data_ptr(), None, st.cuda_stream))
+            torch.cuda.synchronize()
+            for g, r in zip(got, ref):
+                assert torch.equal(g.view(torch.int32), r.view(torch.int32)), trial
+    finally:
+        sc.close()
+
+
 def test_adjoint_row_bands_sum_to_full(scenes):
     from inverse_path_tracer_amd.distributed import shard_rows
 
