@@ -110,11 +110,17 @@ constexpr int kMaxAdjBounces = 62;
 // (profiles/r04/unbounded_pmc_r04g.txt) -- and the unbounded adjoint took 1.7x
 // the unbounded forward.  Now the first IPT_ADJU_LDS_SLOTS slots of every lane
 // are in LDS (a path of up to 8 vertices never touches global memory) and the
-// rest of the ring is global: as many slots as IPT_ADJU_RING_MB (64 MB) holds
-// for the launch's resident lanes, up to IPT_ADJU_RING slots in all -- 24 at
-// C3 (8 + 16, 327 680 lanes), 31 for the north-star BVH instance (4 + 27,
-// fewer resident lanes; 32 vs 24 slots there: 8.67 -> 8.34 ms,
-// profiles/r04/variants_adju_ushift_ring_r04m.log).  Chunks are aligned to the ring: a path of K vertices is swept in chunks
+// rest of the ring is global: as many slots as IPT_ADJU_RING_MB (256 MB) holds
+// for the launch's resident lanes, up to IPT_ADJU_RING = 63 slots in all (63
+// at C3: 7 + 56, 327 680 lanes).  The ring's size is what bounds the
+// launch's tail: a path longer than the ring replays from its camera ray, and
+// the longest paths of a launch (~65 vertices in 16.8 M Russian-roulette
+// paths) then run alone at its end -- a 24-slot ring (64 MB) left the average
+// wave idle for a quarter of the C3 launch; 63 slots: C3 4.32 -> 4.08 ms,
+// Cornell 3.26 -> 3.08, north star 8.21 -> 8.00
+// (profiles/r04/variants_adju_rings_r04x.log).  Only the slots a path reaches
+// are ever written (the AoS layout below), so the HBM traffic follows the
+// path lengths, not the allocation.  Chunks are aligned to the ring: a path of K vertices is swept in chunks
 // [j R, min((j+1) R, K)), R = ring slots, the last one straight after the
 // first pass (its prefix throughput captured there at vertex j R), every
 // earlier one after a replay from the camera ray to its end (K = 30, R = 24:
@@ -126,10 +132,17 @@ constexpr int kMaxAdjBounces = 62;
 #define IPT_ADJU_SHIFTED_CHAIN 0
 #endif
 #ifndef IPT_ADJU_RING
-#define IPT_ADJU_RING 32
+#define IPT_ADJU_RING 63
 #endif
 #ifndef IPT_ADJU_RING_MB
-#define IPT_ADJU_RING_MB 64
+#define IPT_ADJU_RING_MB 256
+#endif
+// LDS ring slots only while the workgroup's LDS stays under this (bytes): at
+// equal occupancy (5 blocks/CU) scenes/0's unbounded adjoint ran 4.33 ms with
+// 8 slots (32.2 KB) and 4.10 with 6 (26.1 KB), Cornell's 3.26 with 8 (30.0 KB)
+// and 3.40 with 6 (profiles/r04/envab_adjulds_r04w.log, _r04x.log)
+#ifndef IPT_ADJU_LDS_CAP
+#define IPT_ADJU_LDS_CAP (31 * 1024)
 #endif
 #ifndef IPT_ADJU_LDS_SLOTS
 #define IPT_ADJU_LDS_SLOTS 8
@@ -2526,7 +2539,7 @@ int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const f
                                                                            kBlock, base + k * per)
                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, trace_kernel<MODE_ADJU, false, false>,
                                                                            kBlock, base + k * per));
-          if (o >= occ0) best = k;
+          if (o >= occ0 && base + k * per <= IPT_ADJU_LDS_CAP) best = k;
         }
         s->adju_base = base;
         s->adju_nl = best;
