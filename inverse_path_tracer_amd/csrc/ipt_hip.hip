@@ -2424,6 +2424,9 @@ int gpu_pixel_mean_sm(const float *samples_dev, int64_t npix, int spp, float *hd
 #ifndef IPT_FUSED_MEAN
 #define IPT_FUSED_MEAN 1
 #endif
+#ifndef IPT_FUSED_GRAB_SAMPLES  // samples handed out per counter grab (at least)
+#define IPT_FUSED_GRAB_SAMPLES 256
+#endif
 #ifndef IPT_FUSED_WAVE_BYTES
 #define IPT_FUSED_WAVE_BYTES 6144
 #endif
@@ -2454,7 +2457,7 @@ static FusedShape fused_shape(const RenderParams &p, bool bvh) {
   // a grab hands out >= 256 samples (small groups -- spp > 128, or long
   // paths -- would otherwise grab per pixel: the legacy 100-spp createImage
   // issued 250 000 counter atomics, 8 MB of memory-side writes per frame)
-  const int per_grab = std::min(8, (256 + g * p.spp - 1) / (g * p.spp));
+  const int per_grab = std::min(8, (IPT_FUSED_GRAB_SAMPLES + g * p.spp - 1) / (g * p.spp));
   return {slots, g, per_grab};
 }
 
