@@ -66,7 +66,8 @@ void setMaterials(void *scenePtr, float *materials);
  * row_step 1 = a contiguous band, row_step = world = a rank's interleaved
  * share); images and sample buffers hold those rows, in that order.
  * ABI 2 added row_step; ABI 3 dropped the quantised-node export of
- * ipt_scene_export_wide (ipt_abi_version).  Bindings must check the version
+ * ipt_scene_export_wide; ABI 4 added ipt_debug_fail_launches
+ * (ipt_abi_version).  Bindings must check the version
  * before passing this struct. */
 typedef struct ipt_params {
   int32_t width, height, spp, max_bounces;
@@ -77,13 +78,19 @@ typedef struct ipt_params {
 
 const char *ipt_last_error(void);
 void ipt_clear_error(void);
-int ipt_abi_version(void);            /* 3 */
+int ipt_abi_version(void);            /* 4 */
 int ipt_device_count(void);
 /* Diagnostic: bitwise self-test of the kernels' in-range sqrt/division cores
  * against the IEEE operations over n random operands per test; counts[8]
  * receives mismatch counts (0 expected; counts[6] is the number of unit()
  * fast-path hits, not a mismatch).  No reference counterpart. */
 int ipt_selftest_math(uint64_t n, uint64_t seed, uint64_t *counts);
+/* Diagnostic (tests): the next n trace-kernel launches fail with an error
+ * just before their kernel is enqueued -- after the launch's chunk counters
+ * and scratch are allocated.  A later launch on the same stream must be
+ * unaffected (the counters reset themselves on the device).  No reference
+ * counterpart. */
+void ipt_debug_fail_launches(int n);
 
 /* Legacy-symbol configuration (defaults 500, 500, 100, -1, seed -1 = time). */
 void ipt_legacy_config(int width, int height, int spp, int max_bounces, int64_t seed);

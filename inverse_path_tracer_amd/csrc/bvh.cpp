@@ -52,7 +52,10 @@ constexpr double kCostNode = 1.0, kCostPair = 1.0;
 // box's surface area (almost every ray reaches them: room walls) are tested
 // by the unrolled brute-force pair loop ahead of the traversal, up to 2 *
 // kBigPairs of them, instead of sitting in leaves that every ray visits.
-constexpr double kBigFrac = 1.0 / 64;  // 1/32 left the cube of the north-star scene in the tree: fwd 5.27 -> 4.50 ms at 1/64 (profiles/r02_bigfrac_ab.log)
+#ifndef IPT_BVH_BIGFRAC  // (make variant DEFS=-DIPT_BVH_BIGFRAC=... for A/B timing)
+#define IPT_BVH_BIGFRAC (1.0 / 64)
+#endif
+constexpr double kBigFrac = IPT_BVH_BIGFRAC;  // 1/32 left the cube of the north-star scene in the tree: fwd 5.27 -> 4.50 ms at 1/64 (profiles/r02_bigfrac_ab.log)
 constexpr int kBigPairs = 16;  // = ipt_device.h kSmallPairs
 
 struct Box {
@@ -444,8 +447,8 @@ std::vector<uint32_t> shadow_occluder_masks(const HostScene &S, const std::vecto
 // 8 at a time (one triangle per lane), so a leaf of 8 costs one round -- one
 // dependent load -- where the binary SAH's leaves of ~2 (its cost counts
 // pairs) cost a node level each.  Leaves are re-laid as single TriIsect
-// records (<= 16 per leaf).  IPT_WIDE_LEAF_TRIS (environment, scene load)
-// overrides the bound; 0 keeps the binary leaves.  North-star scene: 81 wide
+// records (<= 16 per leaf).  IPT_WIDE_LEAF_TRIS (a build-time define, make
+// variant) sets the bound; 0 keeps the binary leaves.  North-star scene: 81 wide
 // nodes of depth 4 -> 73 of depth 3, 214 leaves of 6 triangles on average;
 // forward 3.843 -> 3.782 ms, adjoint 4.698 -> 4.623 (bound 16: 4.23 / 5.02,
 // the leaves' boxes grow; profiles/r04/envab_wideleaf_r04n.log).
@@ -453,8 +456,7 @@ std::vector<uint32_t> shadow_occluder_masks(const HostScene &S, const std::vecto
 #define IPT_WIDE_LEAF_TRIS 8
 #endif
 static bool build_wide(HostScene *S) {
-  const char *wl = std::getenv("IPT_WIDE_LEAF_TRIS");
-  const int fat = std::min(16, std::max(0, wl ? std::atoi(wl) : IPT_WIDE_LEAF_TRIS));
+  const int fat = std::min(16, std::max(0, (int)IPT_WIDE_LEAF_TRIS));
   // triangles of a binary child code (leaf: its pairs' real triangles)
   std::vector<int> tris_of_node(S->bvh_nodes.size(), -1);
   std::function<int(int)> count = [&](int code) -> int {
@@ -624,9 +626,7 @@ bool build_bvh(HostScene *S) {
   {
     Box all;
     for (const Prim &p : B.prims) all.grow(p.box);
-    // IPT_BVH_BIGFRAC (A/B timing only) overrides the threshold
-    const char *bf = std::getenv("IPT_BVH_BIGFRAC");
-    const double lim = (bf ? std::atof(bf) : kBigFrac) * all.area();
+    const double lim = kBigFrac * all.area();
     std::vector<size_t> cand;
     for (size_t k = 0; k < B.prims.size(); ++k)
       if (B.prims[k].box.area() >= lim) cand.push_back(k);

@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -46,6 +47,12 @@ namespace ipt {
 static thread_local std::string g_gpu_err;
 void gpu_set_error(const std::string &e) { g_gpu_err = e; }
 const char *gpu_last_error() { return g_gpu_err.c_str(); }
+// ipt_debug_fail_launches(n): the next n trace launches fail just before
+// their kernel is enqueued (after the chunk counters and the launch's scratch
+// are allocated) -- the tests' way to check that a failed launch leaves
+// nothing behind that a later launch on the stream depends on
+static std::atomic<int> g_fail_launches{0};
+void gpu_debug_fail_launches(int n) { g_fail_launches.store(n > 0 ? n : 0); }
 
 #define HIP_TRY(expr)                                                                        \
   do {                                                                                       \
@@ -150,6 +157,9 @@ constexpr int kMaxAdjBounces = 62;
 #ifndef IPT_ADJU_LDS_SLOTS_BVH
 #define IPT_ADJU_LDS_SLOTS_BVH 4
 #endif
+#ifndef IPT_ADJU_LDS_SLOTS_FIXED
+#define IPT_ADJU_LDS_SLOTS_FIXED -1
+#endif
 constexpr int kAdjuRing = IPT_ADJU_RING;
 // Dynamic work distribution across the waves of a launch (TraceArgs::chunk):
 // static per-wave ranges left each launch's tail to the waves whose pixels
@@ -187,6 +197,10 @@ constexpr int kBvhMinTris = IPT_BVH_MIN_TRIS;
 #endif
 constexpr int kBvhLdsNodeBytes = IPT_BVH_LDS_KB * 1024;  // stage the whole tree in LDS up to 512 nodes
 
+// XCD regions (TraceArgs::nreg, region_count): off in the shipped library
+#ifndef IPT_REGIONS
+#define IPT_REGIONS 1
+#endif
 struct TraceArgs {
   int W, H, spp, max_bounces;
   uint64_t seed;
@@ -260,12 +274,15 @@ struct TraceArgs {
   // chunk_small (units: work items, or pixels in MODE_FWDM), so a launch ends
   // on small chunks and its waves run dry close together (chunk_range)
   uint32_t chunk_small, chunk_big_n;
+  // the launch's grab counters (one word per material set or XCD region).
+  // Each wave grabs until one grab fails, so a word ends a launch at
+  // `grabs` (launch_grabs: a function of the launch's shape, like the chunk
+  // sizes); the wave whose grab returns grabs - 1 zeroes the word.  Each
+  // launch on a stream thus starts from zeroed counters in stream order -- no
+  // host-side copy of device state, no memset launch per launch, no extra
+  // atomic (a count of finished waves cost 2% on the adjoints)
   uint32_t *chunk_ctr;
-  // value of every set's counter when this launch starts: the counters are
-  // never reset (no memset launch per launch) -- a launch grabs exactly
-  // max(chunks - waves, 0) + waves times per set (each wave grabs until one
-  // grab fails), so the host knows the next launch's base (stream_counters)
-  uint32_t chunk_base;
+  uint32_t grabs;
   // small scenes: acceptance boxes of the pairs (culled shadow casts)
   const PairBox2 *pboxes;
   // small scenes: potential occluders per (source triangle, emitter), nT*nE
@@ -294,11 +311,11 @@ struct TraceArgs {
   // image) are read into ONE XCD's L2 instead of all eight (placement only
   // changes speed, never a result).  Region r is the launch with row0 =
   // reg_row0[r], row_step * nreg, reg_npix[r] pixels (Lemire constant
-  // reg_m_npix[r]), its own chunk counter (chunk_ctr[r]) and base, and
-  // reg_nb[r] big chunks (guided instances).
+  // reg_m_npix[r]), its own chunk counter (chunk_ctr[r]) and reg_nb[r] big
+  // chunks (guided instances).
   int nreg;
   int reg_row0[8];
-  uint32_t reg_base[8], reg_nb[8];
+  uint32_t reg_nb[8], reg_grabs[8];
   uint64_t reg_npix[8], reg_m_npix[8];
 };
 static_assert(alignof(TraceArgs) == 8, "TraceArgs sits right after the ten 8-B scene pointers in the kernarg segment");
@@ -308,14 +325,14 @@ static_assert(alignof(TraceArgs) == 8, "TraceArgs sits right after the ten 8-B s
 // a wave-uniform offset -- indexing a register copy of the arrays miscompiles)
 template <class SRC>
 __device__ __forceinline__ void region_view(TraceArgs &v, const SRC *src, int reg) {
-  if (v.nreg > 1) {
+  if (IPT_REGIONS > 1 && v.nreg > 1) {  // (regions are compiled in by variant builds only)
     v.row0 = src->reg_row0[reg];
     v.row_step *= v.nreg;
     v.npix = src->reg_npix[reg];
     v.n_samples = v.npix * (uint64_t)v.spp;
     v.m_npix = src->reg_m_npix[reg];
-    v.chunk_base = src->reg_base[reg];
     v.chunk_big_n = src->reg_nb[reg];
+    v.grabs = src->reg_grabs[reg];
   }
 }
 
@@ -375,6 +392,12 @@ __device__ __forceinline__ void chunk_range(const TraceArgs &a, uint64_t g, uint
     len = a.chunk_small;
   }
   end = start + len < units ? start + len : units;
+}
+
+// The failed grab that returned c: the launch's last grab of that word
+// (TraceArgs::grabs) zeroes it.
+__device__ __forceinline__ void grab_failed(uint32_t *word, uint32_t c, uint32_t grabs) {
+  if (c + 1u == grabs) __hip_atomic_store(word, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // global pixel index (r * W + c) of this launch's work item w
@@ -943,8 +966,6 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       // G slots are free
       if (issued && !exhausted && (uint32_t)__popc(sfree) >= G) {
         if (pl0 >= pl1) {
-          // (a wave whose own chunk is past the end grabs once, as in the
-          // unfused protocol: every wave's last grab fails, TraceArgs::chunk_base)
           bool own = false;
           if (!started) {
             started = true;
@@ -953,8 +974,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           }
           if (!own) {
             uint32_t c = 0;
-            if (lane == 0) c = atomicAdd(a.chunk_ctr + set, 1u) - a.chunk_base;
-            chunk_range<BVH>(a, nwaves + (uint32_t)__builtin_amdgcn_readfirstlane((int)c), a.npix, pl0, pl1);  // lane 0 (full exec here)
+            if (lane == 0) c = atomicAdd(a.chunk_ctr + set, 1u);
+            c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);  // lane 0 (full exec here)
+            chunk_range<BVH>(a, nwaves + c, a.npix, pl0, pl1);
+            if (pl0 >= a.npix && lane == 0) grab_failed(a.chunk_ctr + set, c, a.grabs);
           }
         }
         if (pl0 < a.npix) {
@@ -984,7 +1007,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       // (profiles/r02_variants_chunk_*.log): 8 counters on separate lines
       // with stealing and a grab prefetched one chunk ahead were both slower.
       uint32_t c = 0;
-      if (lane == 0) c = atomicAdd(a.chunk_ctr + set + reg, 1u) - a.chunk_base;
+      if (lane == 0) c = atomicAdd(a.chunk_ctr + set + reg, 1u);
       c = (uint32_t)__shfl((int)c, 0);
       uint64_t start, stop;
       chunk_range<BVH>(a, nwaves + c, a.n_samples, start, stop);
@@ -993,6 +1016,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         end = stop;
       } else {
         exhausted = true;
+        if (lane == 0) grab_failed(a.chunk_ctr + set + reg, c, a.grabs);
       }
     }
     // ---- refill finished lanes from the wave's range (ballot + mbcnt)
@@ -1736,13 +1760,12 @@ struct GpuScene {
   size_t pick_tail[24] = {0};  // ... and the per-block tail (fused pixel mean slots) behind it
   int pick_opt[24] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1,
                       -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
-  // dynamic-chunk counters per (stream, number of sets): zeroed once, then
-  // advanced by every launch by a known amount (TraceArgs::chunk_base)
+  // dynamic-chunk counters per stream (stream_counters): `words` grab words,
+  // zeroed once; every launch leaves them zero (TraceArgs::chunk_ctr)
   struct Counters {
     hipStream_t stream;
     int words;
     uint32_t *dev;
-    std::vector<uint32_t> base;  // per counter word
   };
   std::vector<Counters> counters;
   std::mutex counters_mu;
@@ -1914,6 +1937,9 @@ static int check_params(const GpuScene *s, const RenderParams &p) {
   return 0;
 }
 
+#ifndef IPT_DEBUG_GRID
+#define IPT_DEBUG_GRID 0
+#endif
 template <int MODE, bool SPEC, bool BVH>
 static int resident_grid(GpuScene *s, size_t lds_bytes, int *grid) {
   const int slot = MODE * 4 + (SPEC ? 2 : 0) + (BVH ? 1 : 0);
@@ -1928,7 +1954,7 @@ static int resident_grid(GpuScene *s, size_t lds_bytes, int *grid) {
     }
     s->grid[slot] = per_cu * cus;
     s->grid_lds[slot] = lds_bytes;
-    if (std::getenv("IPT_DEBUG_GRID"))
+    if (IPT_DEBUG_GRID)  // (make variant DEFS=-DIPT_DEBUG_GRID=1)
       std::fprintf(stderr, "[ipt] trace_kernel<%d,%d,%d>: %zu B LDS/block, %d blocks/CU x %d CUs\n", MODE, (int)SPEC,
                    (int)BVH, lds_bytes, per_cu, cus);
   }
@@ -1998,7 +2024,7 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.chunk_small = 0;
   a.chunk_big_n = 0;
   a.chunk_ctr = nullptr;
-  a.chunk_base = 0;
+  a.grabs = 0;
   a.pboxes = s->pboxes;
   a.pomask = s->host.nE > 0 ? s->pomask : nullptr;
   a.big_pomask = nullptr;  // set with the other BVH fields (bvh_lds)
@@ -2014,7 +2040,7 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.nreg = 1;
   for (int r = 0; r < 8; ++r) {
     a.reg_row0[r] = 0;
-    a.reg_base[r] = a.reg_nb[r] = 0;
+    a.reg_nb[r] = a.reg_grabs[r] = 0;
     a.reg_npix[r] = a.reg_m_npix[r] = 0;
   }
   a.mean_off = 0;
@@ -2080,53 +2106,54 @@ struct StreamScratch {
   }
 };
 
-// The chunk counters of a launch with `sets` material sets on stream `st`:
-// allocated and zeroed once per (stream, sets) and never reset -- each launch
-// adds exactly grabs_per_set (launch_chunks) to every set's counter
-// (TraceArgs::chunk_base), so the host hands out the base this launch starts
-// from and, once the launch is enqueued, advances it (*cnt; a launch that
-// fails to enqueue never runs and must not move the base).  Launches on one
-// stream run in order; other streams get their own counters.  *lk holds the
-// scene's counter lock until the caller has enqueued the launch, so host
-// threads sharing a stream enqueue in the order of their bases.  A launch
-// captured into a graph (replayed without this host step) gets fresh zeroed
-// counters of its own instead (*scratch, freed behind it; *cnt = nullptr).
-// `words` counter words: one per material set (scene batch) or per XCD
-// region (TraceArgs::nreg); *cnt->base[w] is word w's value when this launch
-// starts (all zero for a captured launch, *cnt = the capture's throwaway).
-static int stream_counters(GpuScene *s, hipStream_t st, int words, uint32_t **out, void **scratch,
-                           GpuScene::Counters **cnt, GpuScene::Counters *cap_cnt, std::unique_lock<std::mutex> *lk) {
-  *cnt = nullptr;
+// The chunk counters of launches on stream `st` with `words` grab words:
+// one buffer per (scene, stream), allocated and zeroed (on `st`, in stream
+// order) at the stream's first launch and grown when a launch needs more
+// words.  Every launch leaves them zeroed
+// (TraceArgs::chunk_ctr), so the host keeps no copy of device state: a launch
+// that fails before or after enqueueing changes nothing the next one depends
+// on, and any kind of launch (single set, regions, scene batch) may follow any
+// other on the stream.  Launches on one stream run in order; other streams
+// get their own buffers.  A launch captured into a graph gets a zeroed buffer
+// of its own inside the graph (*scratch, freed behind it), so a replay never
+// shares words with launches on the capturing stream.
+static int stream_counters(GpuScene *s, hipStream_t st, int words, uint32_t **out, void **scratch) {
+  const size_t bytes = (size_t)words * sizeof(uint32_t);
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   HIP_TRY(hipStreamIsCapturing(st, &cap));
   if (cap != hipStreamCaptureStatusNone) {
-    HIP_TRY(hipMallocAsync(scratch, (size_t)words * sizeof(uint32_t), st));
-    HIP_TRY(hipMemsetAsync(*scratch, 0, (size_t)words * sizeof(uint32_t), st));
+    HIP_TRY(hipMallocAsync(scratch, bytes, st));
+    HIP_TRY(hipMemsetAsync(*scratch, 0, bytes, st));
     *out = (uint32_t *)*scratch;
-    cap_cnt->words = words;
-    cap_cnt->base.assign((size_t)words, 0u);
-    *cnt = cap_cnt;
     return 0;
   }
-  *lk = std::unique_lock<std::mutex>(s->counters_mu);
+  std::lock_guard<std::mutex> lk(s->counters_mu);
   GpuScene::Counters *c = nullptr;
   for (auto &e : s->counters)
-    if (e.stream == st && e.words == words) c = &e;
-  if (!c) {
+    if (e.stream == st) c = &e;
+  if (c && c->words < words) {  // grow (after the launches queued on the old buffer)
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipFree(c->dev));
+    c->dev = nullptr;
+    c->words = 0;
+  }
+  if (!c || c->dev == nullptr) {
+    const int w = std::max(words, 16);
     uint32_t *dev = nullptr;
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&dev), (size_t)words * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&dev), (size_t)w * sizeof(uint32_t)));
     // zeroed ON the launch stream: a blocking hipMemset goes to the null
     // stream, which a non-blocking stream (every torch stream) does not wait
-    // for -- behind queued null-stream work the zeroing landed after this
-    // stream's first launch had advanced the counter, every later launch's
-    // base was off and its waves ran dry early (frames in flight rendered
-    // only part of the image; caught by bench.py's bitwise check)
-    HIP_TRY(hipMemsetAsync(dev, 0, (size_t)words * sizeof(uint32_t), st));
-    s->counters.push_back({st, words, dev, std::vector<uint32_t>((size_t)words, 0u)});
-    c = &s->counters.back();
+    // for (round 4's race)
+    HIP_TRY(hipMemsetAsync(dev, 0, (size_t)w * sizeof(uint32_t), st));
+    if (c) {
+      c->dev = dev;
+      c->words = w;
+    } else {
+      s->counters.push_back({st, w, dev});
+      c = &s->counters.back();
+    }
   }
   *out = c->dev;
-  *cnt = c;
   return 0;
 }
 
@@ -2136,29 +2163,15 @@ static int stream_counters(GpuScene *s, hipStream_t st, int words, uint32_t **ou
 // bytes 25.9 -> 3.8 MB per launch -- every XCD's L2 no longer pulls the whole
 // adjoint image -- but cost 1.6% time (C2 adjoint 1.911 -> 1.942 ms, the
 // unbounded one 4.01 -> 4.15): a region's waves cannot help the region that
-// ends last.  Off by default (IPT_REGIONS = 1); the environment variable of
-// that name (a power of two <= 8) turns them on for A/B timing.
-#ifndef IPT_REGIONS
-#define IPT_REGIONS 1
-#endif
+// ends last.  Off in the shipped library (IPT_REGIONS = 1); `make variant
+// DEFS=-DIPT_REGIONS=8` builds them for A/B timing.
 template <int MODE>
 static int region_count(const TraceArgs &a, int grid) {
   if (!(is_badj<MODE>() || MODE == MODE_ADJU || MODE == MODE_GRAPH) || a.nscenes > 1 || a.fused) return 1;
   int R = IPT_REGIONS;
-  if (const char *e = std::getenv("IPT_REGIONS")) R = std::max(1, std::min(8, std::atoi(e)));
   const uint64_t rows = a.W > 0 ? a.npix / (uint64_t)a.W : 0;
   while (R > 1 && ((uint64_t)R > rows || grid % R != 0 || (R & (R - 1)) != 0)) R >>= 1;
   return R;
-}
-
-// Chunks of a launch exactly as the kernel enumerates them (chunk_range):
-// guided instances (BVH) hand out nb chunks of c units and then chunks of
-// `small`; the others only chunks of c (they ignore chunk_small).  Each wave
-// grabs until one grab fails, so a set's counter moves by
-// max(chunks - waves, 0) + waves (TraceArgs::chunk_base).
-static uint64_t launch_chunks(bool guided, uint64_t units, uint64_t c, uint64_t small, uint64_t nb) {
-  if (!guided) return (units + c - 1) / c;
-  return nb + (units - nb * c + small - 1) / small;
 }
 
 // Guided chunk sizes (TraceArgs::chunk_big_n), BVH instances: a launch hands
@@ -2171,18 +2184,26 @@ static uint64_t launch_chunks(bool guided, uint64_t units, uint64_t c, uint64_t 
 // (C2 1/8 share 0.278 -> 0.297 ms at 2 per wave: the fused render's 64-sample
 // chunks outrun its two LDS slots, and each extra grab is an atomic round
 // trip the wave waits for), so their instances keep fixed chunks
-// (profiles/r03/envab_r03j.log).  The environment variable of the same name
-// overrides the count (A/B timing).
+// (profiles/r03/envab_r03j.log).
 #ifndef IPT_GUIDED_TAIL
 #define IPT_GUIDED_TAIL 4
 #endif
+
+// Grabs of one counter word in a launch (a set's or a region's; units, big
+// chunks and waves as chunk_range and the kernel's loop see them): chunks 0 ..
+// rw-1 are the waves' own, each later chunk is taken by one successful grab,
+// and every wave ends with exactly one failed grab -- the non-fused loop
+// grabs when its range is used up and stops at the first chunk past the end;
+// the fused loop grabs when its chunk is used up, or at once when its own
+// chunk is past the end.  Guided instances (BVH) hand out nb chunks of c
+// units and then chunks of `small`, the others only chunks of c.
+static uint32_t launch_grabs(bool guided, uint64_t units, uint64_t c, uint64_t small, uint64_t nb, uint64_t rw) {
+  const uint64_t chunks = guided ? nb + (units - nb * c + small - 1) / small : (units + c - 1) / c;
+  return (uint32_t)((chunks > rw ? chunks - rw : 0) + rw);
+}
 #ifndef IPT_DYN_SMALL_CHUNK
 #define IPT_DYN_SMALL_CHUNK 64
 #endif
-static int guided_tail() {
-  const char *e = std::getenv("IPT_GUIDED_TAIL");
-  return e ? std::max(0, std::atoi(e)) : IPT_GUIDED_TAIL;
-}
 
 template <int MODE, bool SPEC, bool BVH>
 static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float *kd_dev, float *out, const float *adj,
@@ -2201,13 +2222,8 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
   }
   b.chunk = 0;
   b.chunk_ctr = nullptr;
-  b.chunk_base = 0;
   b.nreg = 1;
   StreamScratch cap_ctr;  // only for a launch captured into a graph
-  GpuScene::Counters cap_cnt{st, 0, nullptr, {}};
-  std::unique_lock<std::mutex> ctr_lock;  // released after the launch is enqueued
-  GpuScene::Counters *ctr = nullptr;     // advanced by grabs[] once the launch is enqueued
-  uint64_t grabs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (IPT_DYN_CHUNKS) {
     // ~IPT_DYN_CHUNKS_PER_WAVE chunks per wave, a multiple of 64 items, 64..4096
     const uint64_t waves = (uint64_t)(a.nscenes > 1 ? b.bps : grid) * (kBlock / 64);
@@ -2224,13 +2240,12 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
       small = std::min<uint64_t>(c, std::max<uint64_t>(1, 64 / (uint64_t)a.spp));
       units = a.npix;
     }
-    // guided sizes: the last ~guided_tail() small chunks per wave end the launch
+    // guided sizes: the last ~IPT_GUIDED_TAIL small chunks per wave end the launch
     // (non-guided instances: one size, chunk_small = chunk and no big-chunk count)
     if (!BVH) small = c;
     b.chunk = (uint32_t)c;
     b.chunk_small = (uint32_t)small;
-    // per XCD region (one region = the whole launch): its units, big chunks
-    // and grabs (each of its waves grabs until one grab fails: TraceArgs::chunk_base)
+    // per XCD region (one region = the whole launch): its units and big chunks
     const int R = region_count<MODE>(a, grid);
     const uint64_t rw = waves / (uint64_t)R, rows = a.npix / (uint64_t)a.W;
     for (int r = 0; r < R; ++r) {
@@ -2242,19 +2257,19 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
         b.reg_npix[r] = np;
         b.reg_m_npix[r] = np > 1 ? ~0ull / np + 1 : 0;
       }
-      const uint64_t tail = BVH ? rw * (uint64_t)guided_tail() * small : 0;
+      const uint64_t tail = BVH ? rw * (uint64_t)IPT_GUIDED_TAIL * small : 0;
       const uint64_t nb = BVH ? (ur > tail ? (ur - tail) / c : 0) : 0;
       b.reg_nb[r] = (uint32_t)nb;
-      if (r == 0) b.chunk_big_n = (uint32_t)nb;
-      const uint64_t chunks = launch_chunks(BVH, ur, c, small, nb);
-      grabs[r] = (chunks > rw ? chunks - rw : 0) + rw;
+      b.reg_grabs[r] = launch_grabs(BVH, ur, c, small, nb, rw);
+      if (r == 0) {
+        b.chunk_big_n = (uint32_t)nb;
+        b.grabs = b.reg_grabs[0];
+      }
     }
     b.nreg = R;
     cap_ctr.st = st;
-    if (stream_counters(s, st, a.nscenes > 1 ? a.nscenes : 8, &b.chunk_ctr, &cap_ctr.p, &ctr, &cap_cnt, &ctr_lock))
-      return -1;
-    b.chunk_base = ctr->base[0];  // (a scene batch: every set's counter moves alike)
-    for (int r = 0; r < R; ++r) b.reg_base[r] = ctr->base[(size_t)r];
+    const int words = std::max(a.nscenes, R);
+    if (stream_counters(s, st, words, &b.chunk_ctr, &cap_ctr.p)) return -1;
   }
   StreamScratch grec;  // ADJU: the vertex-record ring (TraceArgs::grec), freed behind the launch
   if (MODE == MODE_ADJU) {  // the ring's global slots
@@ -2267,18 +2282,15 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
     if (grec.alloc(fields * (size_t)(b.rec_cap - b.rec_lds) * b.grec_stride * sizeof(float), st)) return -1;
     b.grec = (float *)grec.p;
   }
+  // (tests: a launch that fails after its counters and scratch are allocated)
+  if (g_fail_launches.load() > 0 && g_fail_launches.fetch_sub(1) > 0) {
+    gpu_set_error("launch failed on request (ipt_debug_fail_launches)");
+    return -1;
+  }
   hipLaunchKernelGGL((trace_kernel<MODE, SPEC, BVH>), dim3(grid), dim3(kBlock), lds, st, b, s->isect, s->pairs, s->geom,
                      s->mat, kd_dev ? kd_dev : s->kd, s->emit_tri, s->emit_cdf, s->emit_pmf, out, adj, grad, target,
                      edges);
   HIP_TRY(hipGetLastError());
-  if (ctr) {  // (mod 2^32: the kernel subtracts in uint32)
-    if (b.nreg > 1)  // region r's word
-      for (int r = 0; r < b.nreg; ++r) ctr->base[(size_t)r] += (uint32_t)grabs[r];
-    else if (a.nscenes > 1)  // every set's word
-      for (uint32_t &w : ctr->base) w += (uint32_t)grabs[0];
-    else
-      ctr->base[0] += (uint32_t)grabs[0];
-  }
   return 0;
 }
 
@@ -2419,8 +2431,9 @@ int gpu_pixel_mean_sm(const float *samples_dev, int64_t npix, int spp, float *hd
 // <= 8 bounces) or four (longer or unbounded paths: a few long paths then
 // still leave the next groups their slots -- simulated lane use >= 99% for
 // the reference's Russian roulette).  The index math needs
-// < 2^32 samples per frame.  IPT_RENDER_TWO_KERNEL=1 (environment) forces the
-// unfused path (A/B timing, tests).
+// < 2^32 samples per frame.  (The unfused path stays reachable through
+// ipt_render_samples_sm_dev + ipt_pixel_mean_sm_dev; `make variant
+// DEFS=-DIPT_FUSED_MEAN=0` builds a library without the fused render.)
 #ifndef IPT_FUSED_MEAN
 #define IPT_FUSED_MEAN 1
 #endif
@@ -2433,19 +2446,25 @@ int gpu_pixel_mean_sm(const float *samples_dev, int64_t npix, int spp, float *hd
 struct FusedShape {
   int slots, group, per_grab;  // per_grab: groups per chunk (counter grab)
 };
-// BVH scenes keep the two-kernel render unless IPT_FUSED_BVH=1 (environment,
-// A/B timing): their LDS already holds the tree stage, and slots beyond
-// IPT_FUSED_BVH_WAVE_BYTES per wave cost residency.
+// BVH scenes keep the two-kernel render unless the library is built with
+// IPT_FUSED_BVH=1 (make variant, A/B timing): their LDS already holds the
+// tree stage, and slots beyond IPT_FUSED_BVH_WAVE_BYTES per wave cost
+// residency (north-star 3.82 -> 4.10 ms fused,
+// profiles/r04/envab_fusedbvh_r04e.log).
+#ifndef IPT_FUSED_BVH
+#define IPT_FUSED_BVH 0
+#endif
+#ifndef IPT_FUSED_BVH_WAVE_BYTES
+#define IPT_FUSED_BVH_WAVE_BYTES 3072
+#endif
 static FusedShape fused_shape(const RenderParams &p, bool bvh) {
   const FusedShape none = {0, 0, 0};
-  if (!IPT_FUSED_MEAN || !IPT_DYN_CHUNKS || std::getenv("IPT_RENDER_TWO_KERNEL")) return none;
+  if (!IPT_FUSED_MEAN || !IPT_DYN_CHUNKS) return none;
   if ((uint64_t)p.width * (uint64_t)p.height * (uint64_t)p.spp > 0xffffffffull || p.spp > 256) return none;
   int bytes = IPT_FUSED_WAVE_BYTES;
   if (bvh) {
-    const char *on = std::getenv("IPT_FUSED_BVH");
-    if (!on || std::atoi(on) == 0) return none;
-    const char *b = std::getenv("IPT_FUSED_BVH_WAVE_BYTES");
-    bytes = b ? std::max(0, std::atoi(b)) : 3072;
+    if (!IPT_FUSED_BVH) return none;
+    bytes = IPT_FUSED_BVH_WAVE_BYTES;
   }
   const int slots = std::min(16, bytes / (12 * p.spp));
   const bool long_paths = p.max_bounces < 0 || p.max_bounces > 8;
@@ -2518,15 +2537,14 @@ int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const f
                       (size_t)kBlock * sizeof(uint32_t);  // + the sweep's owner markers
   if (unbounded) {
     // ring slots in LDS: up to IPT_ADJU_LDS_SLOTS (brute force) or
-    // IPT_ADJU_LDS_SLOTS_BVH, as many as cost no resident workgroup (the
-    // environment variable IPT_ADJU_LDS_SLOTS fixes the count, A/B timing);
-    // the rest of the ring in global memory
+    // IPT_ADJU_LDS_SLOTS_BVH, as many as cost no resident workgroup (a
+    // variant built with IPT_ADJU_LDS_SLOTS_FIXED >= 0 fixes the count, A/B
+    // timing); the rest of the ring in global memory
     a.rec_cap = kAdjuRing;
     const bool bvh = use_bvh(s);
     int nl = bvh ? IPT_ADJU_LDS_SLOTS_BVH : IPT_ADJU_LDS_SLOTS;
-    const char *e = std::getenv("IPT_ADJU_LDS_SLOTS");
-    if (e) {
-      nl = std::atoi(e);
+    if (IPT_ADJU_LDS_SLOTS_FIXED >= 0) {
+      nl = IPT_ADJU_LDS_SLOTS_FIXED;
     } else if (!bvh) {
       const size_t per = fields * kBlock * sizeof(float);
       if (s->adju_base != base) {  // cached per scene for this LDS base

@@ -160,13 +160,13 @@ def test_adjoint_six_wave_instance_matches_oracle(scenes, monkeypatch, name, W, 
 
 
 def test_back_to_back_launches_with_ragged_chunks(scenes):
-    """Launches on one stream share the chunk counters, each starting from the
-    base the host advanced by the previous launch's grabs (ipt_hip.hip
-    stream_counters / launch_chunks).  509 x 97 pixels: the fused render's
-    last 8-pixel chunk holds 5 (more than its 4-pixel small chunk) and the
-    adjoint's 789 968 samples leave 80 (more than 64) past the last full
-    128-item chunk, with more chunks than waves -- a host that counted chunks
-    differently from the kernel re-traced a chunk in every later launch."""
+    """Launches on one stream share the chunk counters, which the last wave of
+    each launch zeroes (ipt_hip.hip TraceArgs::ctr_done).  509 x 97 pixels:
+    the fused render's last 8-pixel chunk holds 5 (more than its 4-pixel
+    small chunk) and the adjoint's 789 968 samples leave 80 (more than 64)
+    past the last full 128-item chunk, with more chunks than waves -- round
+    4's host-side count of the grabs had to match the kernel's enumeration
+    exactly, or every later launch re-traced a chunk."""
     P, Q = scenes["scene0"]
     W, H, spp, mb, seed = 509, 97, 16, 4, 21
     adj = np.random.RandomState(8).uniform(-1, 1, (H, W, 3)).astype(np.float32)
@@ -200,6 +200,7 @@ def test_new_stream_behind_busy_null_stream():
     L = N.lib()
     hip = C.CDLL("libamdhip64.so")
     sc = product_scene(CORNELL)
+    raws = []
     try:
         W = H = 256
         ps = [N.make_params(W, H, 64, 4, 5 + i) for i in range(3)]
@@ -216,6 +217,7 @@ def test_new_stream_behind_busy_null_stream():
             # may hand back one whose counters already exist)
             raw = C.c_void_p()
             assert hip.hipStreamCreateWithFlags(C.byref(raw), 1) == 0  # hipStreamNonBlocking
+            raws.append(raw)
             st = torch.cuda.ExternalStream(raw.value)
             got = [torch.full((W * H, 3), float("nan"), device="cuda") for _ in ps]
             torch.cuda.synchronize()
@@ -227,7 +229,124 @@ def test_new_stream_behind_busy_null_stream():
             for g, r in zip(got, ref):
                 assert torch.equal(g.view(torch.int32), r.view(torch.int32)), trial
     finally:
-        sc.close()
+        torch.cuda.synchronize()
+        sc.close()  # (frees the scene's per-stream counters)
+        for raw in raws:
+            hip.hipStreamDestroy(raw)
+
+
+def _stream(hip):
+    import torch
+
+    raw = C.c_void_p()
+    assert hip.hipStreamCreateWithFlags(C.byref(raw), 1) == 0  # hipStreamNonBlocking
+    return raw, torch.cuda.ExternalStream(raw.value)
+
+
+def test_mixed_launch_kinds_share_one_stream(scenes):
+    """Every kind of launch may follow any other on a stream: single-set
+    renders, 8-set scene batches (as many counter words as a single launch
+    has), adjoints and createGraph, interleaved on one fresh stream -- each
+    result equals the same launch alone on its own fresh stream (round 4's
+    counters, keyed by word count with per-word host bases, gave an 8-set
+    batch after a single render stale bases for sets 1..7: ADVICE r4)."""
+    import torch
+
+    from inverse_path_tracer_amd import _native as N
+
+    L = N.lib()
+    hip = C.CDLL("libamdhip64.so")
+    P, _ = scenes["scene0"]
+    W, H, spp, mb, seed = 96, 64, 16, 4, 77
+    S, stride = 8, W * H * spp
+    kd = torch.from_numpy(np.random.RandomState(5).uniform(0, 1, (S, P.nT, 3)).astype(np.float32)).cuda()
+    adj = torch.from_numpy(np.random.RandomState(6).uniform(-1, 1, (S, H, W, 3)).astype(np.float32)).cuda()
+    tgt = torch.from_numpy(np.random.RandomState(7).randint(0, 255, (H, W, 3)).astype(np.uint8)).cuda()
+    p = N.make_params(W, H, spp, mb, seed)
+    pu = N.make_params(W, H, spp, -1, seed + 1)
+    nacc = (P.nT + 1) * P.nT * 8
+
+    def run(kind, st):
+        if kind == "render":
+            o = torch.empty((H * W, 3), device="cuda")
+            N.check(L.ipt_render_dev(P.handle, C.byref(p), kd[3].data_ptr(), o.data_ptr(), None, st))
+        elif kind == "batch":
+            o = torch.empty((S, H * W, 3), device="cuda")
+            N.check(L.ipt_render_batch_dev(P.handle, C.byref(p), S, stride, kd.data_ptr(), o.data_ptr(), st))
+        elif kind == "adjoint":
+            o = torch.zeros((P.nT, 3), device="cuda", dtype=torch.float64)
+            N.check(L.ipt_adjoint_dev(P.handle, C.byref(p), kd[1].data_ptr(), adj[1].data_ptr(), o.data_ptr(), st))
+        elif kind == "adjoint_u":
+            o = torch.zeros((P.nT, 3), device="cuda", dtype=torch.float64)
+            N.check(L.ipt_adjoint_dev(P.handle, C.byref(pu), kd[2].data_ptr(), adj[2].data_ptr(), o.data_ptr(), st))
+        elif kind == "adjoint_batch":
+            o = torch.zeros((S, P.nT, 3), device="cuda", dtype=torch.float64)
+            N.check(L.ipt_adjoint_batch_dev(P.handle, C.byref(p), S, stride, kd.data_ptr(), adj.data_ptr(),
+                                            o.data_ptr(), st))
+        else:  # graph
+            o = torch.zeros(nacc, device="cuda", dtype=torch.float64)
+            N.check(L.ipt_graph_dev(P.handle, C.byref(pu), tgt.data_ptr(), o.data_ptr(), st))
+        return o
+
+    kinds = ["render", "batch", "batch", "adjoint", "render", "adjoint_batch", "graph", "batch", "adjoint_u",
+             "render", "adjoint_batch", "batch"]
+    raws = []
+    try:
+        want = {}
+        for k in sorted(set(kinds)):  # each kind alone on a fresh stream
+            raw, st = _stream(hip)
+            raws.append(raw)
+            want[k] = run(k, st.cuda_stream)
+        torch.cuda.synchronize()
+        raw, st = _stream(hip)
+        raws.append(raw)
+        got = [run(k, st.cuda_stream) for k in kinds]
+        torch.cuda.synchronize()
+        for k, g in zip(kinds, got):
+            w = want[k]
+            if k in ("render", "batch"):
+                assert torch.equal(g.view(torch.int32), w.view(torch.int32)), k
+            else:  # fp64 sums: only the order of the atomics differs
+                np.testing.assert_allclose(g.cpu().numpy(), w.cpu().numpy(), rtol=1e-9, atol=1e-13, err_msg=k)
+    finally:
+        torch.cuda.synchronize()
+        for raw in raws:
+            hip.hipStreamDestroy(raw)
+
+
+def test_failed_launch_leaves_the_stream_usable(scenes):
+    """A launch that fails after its chunk counters and scratch are allocated
+    (ipt_debug_fail_launches: the error comes just before the kernel is
+    enqueued) changes nothing a later launch on the stream depends on: the
+    next render, adjoint and unbounded adjoint on the same stream (the host
+    wrappers' null stream) equal the oracle."""
+    import oracle_lib
+    from inverse_path_tracer_amd import _native as N
+
+    L = N.lib()
+    P, Q = scenes["scene0"]
+    W, H, spp, mb, seed = 64, 48, 8, 4, 31
+    adj = np.random.RandomState(2).uniform(-1, 1, (H, W, 3)).astype(np.float32)
+    for kind in ("render", "adjoint", "adjoint_u"):
+        b = None if kind == "adjoint_u" else mb
+        L.ipt_debug_fail_launches(1)
+        try:
+            with pytest.raises(N.NativeError, match="on request"):
+                if kind == "render":
+                    P.render(W, H, spp, b, seed)
+                else:
+                    P.adjoint(adj, W, H, spp, b, seed)
+        finally:
+            L.ipt_debug_fail_launches(0)
+        if kind == "render":
+            hdr = P.render(W, H, spp, b, seed)
+            s, _ = Q.render_samples(W, H, spp, b, seed)
+            hq, _ = oracle_lib.pixel_mean(s, W * H, spp)
+            assert np.array_equal(bits(hdr.reshape(-1, 3)), bits(hq))
+        else:
+            g = P.adjoint(adj, W, H, spp, b, seed)
+            want = Q.adjoint(W, H, spp, b, seed, adj)
+            np.testing.assert_allclose(g, want, rtol=1e-9, atol=1e-12)
 
 
 def test_adjoint_row_bands_sum_to_full(scenes):

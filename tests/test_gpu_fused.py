@@ -3,8 +3,8 @@ MODE_FWDM): each wave keeps a ring of one-pixel LDS slots and sums a pixel's
 samples in sample order once its last one is in, so the HDR image (and its
 8-bit tonemap) must be bit-identical to the oracle's toneMap over the
 oracle's per-sample radiances (path_trace.cu:186-198) and to the unfused
-two-kernel render (IPT_RENDER_TWO_KERNEL=1: sample buffer +
-pixel_mean_sm_kernel).
+two-kernel render (ipt_render_samples_sm_dev into a sample buffer +
+ipt_pixel_mean_sm_dev).
 
 Cases cover the group shapes gpu_render picks (p pixels per group, p * spp
 <= 256, the ring holding 2 groups for <= 8 bounces and 4 otherwise): spp a
@@ -14,8 +14,6 @@ division path of the item split), long bounded paths and the reference's
 own unbounded estimator (long Russian-roulette paths hold their pixel's slot
 while the ring moves on), row bands and interleaved shares, the BVH
 instance (two-kernel render) and the unfused fallback (spp > 256)."""
-import os
-
 import numpy as np
 import pytest
 
@@ -43,12 +41,22 @@ def scenes(oracle):
             (("cornell", CORNELL), ("scene0", SCENE0), ("northstar", NORTHSTAR))}
 
 
-def two_kernel(fn):
-    os.environ["IPT_RENDER_TWO_KERNEL"] = "1"
-    try:
-        return fn()
-    finally:
-        del os.environ["IPT_RENDER_TWO_KERNEL"]
+def two_kernel(P, W, H, spp, mb, seed, row_begin=0, row_end=None):
+    """The unfused render of the same rows: the per-sample kernel into a
+    sample-major buffer, then the toneMap kernel (flattened HDR image)."""
+    import ctypes as C
+
+    from inverse_path_tracer_amd import _native as N
+
+    L = N.lib()
+    p = N.make_params(W, H, spp, mb, seed, row_begin, row_end)
+    rows = (H if row_end is None else row_end) - row_begin
+    samples = torch.empty((spp * rows * W, 3), device="cuda")
+    hdr = torch.empty((rows * W, 3), device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    N.check(L.ipt_render_samples_sm_dev(P.handle, C.byref(p), None, samples.data_ptr(), st))
+    N.check(L.ipt_pixel_mean_sm_dev(samples.data_ptr(), rows * W, spp, hdr.data_ptr(), None, st))
+    return hdr.cpu().numpy().reshape(-1)
 
 
 @pytest.mark.parametrize("name,W,H,spp,mb,seed", [
@@ -82,7 +90,7 @@ def test_fused_c2_frame_equals_oracle_and_unfused(scenes, oracle):
     hdr = P.render(512, 512, 64, 4, 0)
     want, _, _ = Q.render(512, 512, 64, 4, 0)
     assert np.array_equal(bits(hdr), bits(want))
-    assert np.array_equal(bits(two_kernel(lambda: P.render(512, 512, 64, 4, 0))), bits(hdr))
+    assert np.array_equal(bits(two_kernel(P, 512, 512, 64, 4, 0)), bits(hdr).reshape(-1))
     for r in (0, 5):
         share = P.render(512, 512, 64, 4, 0, r, 512, row_step=8)
         assert np.array_equal(bits(share), bits(hdr[r::8]))
@@ -104,7 +112,7 @@ def test_fused_band_of_c4_shape(scenes):
     a band of a 1024-wide frame: fused == unfused, bitwise."""
     P, _ = scenes["scene0"]
     a = (1024, 1024, 256, 8, 0, 512, 520)
-    assert np.array_equal(bits(P.render(*a)), bits(two_kernel(lambda: P.render(*a))))
+    assert np.array_equal(bits(P.render(*a)).reshape(-1), bits(two_kernel(P, *a)))
 
 
 def test_fused_render_batch_equals_single(scenes):
