@@ -131,7 +131,7 @@ class MaterialOptimizer:
     `flush_every` steps (on every rank) and at the end of each run().
 
     Sample streams: step t of the whole job (n_total scenes over all ranks,
-    default len(tasks)) traces frames [2 t n_total, 2 (t + 1) n_total) of the
+    default max(task index) + 1) traces frames [2 t n_total, 2 (t + 1) n_total) of the
     sample-index space, scene i's forward in frame 2 t n_total + i and its
     adjoint n_total frames later -- so each rank of a scene-parallel split
     traces exactly the one-rank run's samples for its scenes.  A batch is
@@ -143,7 +143,14 @@ class MaterialOptimizer:
                  decorrelate: bool = True, n_total: Optional[int] = None):
         self.tasks, self.W, self.H, self.spp, self.mb = tasks, width, height, spp, max_bounces
         self.tie, self.seed, self.flush_every, self.decorrelate = tie_shared, seed, flush_every, decorrelate
-        self.n_total = len(tasks) if n_total is None else int(n_total)
+        # the job's scene count: the caller's, else max(index) + 1 (a rank
+        # given only the tasks of global scenes b .. b+k-1 must pass the job's n)
+        idx = [t.index for t in tasks]
+        if len(set(idx)) != len(idx):
+            raise ValueError("MaterialOptimizer: task indices must be unique (build_tasks(first_index=...))")
+        self.n_total = (max(idx) + 1 if idx else 0) if n_total is None else int(n_total)
+        if idx and max(idx) >= self.n_total:
+            raise ValueError("MaterialOptimizer: task index %d >= n_total %d" % (max(idx), self.n_total))
         self.frame = width * height * spp
         self.batches = []  # (scene, tasks)
         for t in tasks:
