@@ -234,7 +234,7 @@ double scene_coord_bound(const HostScene &S) {
   return m + 1.0;
 }
 
-int acceptance_box(const TriIsect &T, const TriGeom &G, double r_all, float lo[3], float hi[3]) {
+int acceptance_box(const TriIsect &T, const TriGeom &G, double r_all, float lo[3], float hi[3], double verts[6][3]) {
   const float *fields[5] = {T.c, T.n, T.e0, T.e1, T.e2};
   const int counts[5] = {3, 3, 4, 4, 4};
   for (int f = 0; f < 5; ++f)
@@ -281,6 +281,7 @@ int acceptance_box(const TriIsect &T, const TriGeom &G, double r_all, float lo[3
         for (int a = 0; a < 3; ++a) {
           blo[a] = std::min(blo[a], x[a]);
           bhi[a] = std::max(bhi[a], x[a]);
+          if (verts) verts[2 * j + (s > 0 ? 1 : 0)][a] = x[a];
         }
       }
     }
@@ -601,6 +602,67 @@ static bool build_wide(HostScene *S) {
   return true;
 }
 
+// Two exact, conservative entry tests for the tree (ipt_device.h
+// coop_root_test, tree_skip), computed from the acceptance regions A_w of the
+// tree's triangles (the prisms acceptance_box bounds; convex, their six
+// vertices below):
+//  * bounding sphere: centre = the root box's centre (a float), radius = the
+//    largest distance from it to a vertex of some A_w, padded by 2^-10 R --
+//    over 100x the fp32 error of the kernel's ray-sphere test (|p|, |c| <= R,
+//    squared terms <= 4R^2 with a few roundings of 2^-24 each).  A ray whose
+//    origin is outside the padded sphere and whose line misses it accepts no
+//    tree triangle.
+//  * source plane: a ray leaving a point p that triangle s's test accepted
+//    (|n_s.(p - c_s)| <= h, the acceptance slab) reaches, at any t >= 1e-2
+//    (the test rejects smaller t), points with n_s.(x - c_s) >=
+//    -h + 1e-2 (n_s.d); the computed hit point of a tree triangle w lies
+//    within 2^-23 R of the exact ray point, and inside A_w, where n_s.(x -
+//    c_s) <= M_s = the largest value over all A_w's vertices.  So when
+//    1e-2 (n_s.d) > M_s + h + 2^-23 R, no tree triangle can accept the ray:
+//    tau_s = (M_s + h + 2^-23 R) / 1e-2 + 2e-6 (the fp32 dot's error), the
+//    kernel skips the tree when dot(n_s, d) >= tau_s.  Every tree triangle
+//    behind s's plane -- a convex mesh's own faces seen from any of them, or
+//    an object behind a wall -- gives tau_s < 1; otherwise tau_s = +inf.
+//    (North-star scene: every path and shadow ray leaving the sphere.)
+static void tree_cull(HostScene *S, const std::vector<Prim> &tree, double r_all) {
+  const float inf = std::numeric_limits<float>::infinity();
+  std::vector<double> vx;  // the tree triangles' region vertices, xyz
+  vx.reserve(tree.size() * 18);
+  for (const Prim &p : tree) {
+    float l[3], u[3];
+    double v[6][3];
+    if (acceptance_box(S->isect[(size_t)p.tri], S->geom[(size_t)p.tri], r_all, l, u, v) != 0) continue;
+    for (int k = 0; k < 6; ++k)
+      for (int a = 0; a < 3; ++a) vx.push_back(v[k][a]);
+  }
+  const size_t nv = vx.size() / 3;
+  float c[3];
+  for (int a = 0; a < 3; ++a) c[a] = 0.5f * S->bvh_root_box[a] + 0.5f * S->bvh_root_box[3 + a];
+  double rho2 = 0.0;
+  for (size_t k = 0; k < nv; ++k) {
+    double d2 = 0.0;
+    for (int a = 0; a < 3; ++a) d2 += (vx[3 * k + a] - c[a]) * (vx[3 * k + a] - c[a]);
+    rho2 = std::max(rho2, d2);
+  }
+  const double rho = std::sqrt(rho2) + std::ldexp(r_all, -10);
+  for (int a = 0; a < 3; ++a) S->bvh_sphere[a] = c[a];
+  S->bvh_sphere[3] = round_up(rho * rho * (1.0 + 1e-12));
+  const double h = std::ldexp(3.0 * r_all, -17);
+  S->bvh_src_cull.assign((size_t)S->nT * 4, 0.f);
+  for (int si = 0; si < S->nT; ++si) {
+    const TriIsect &T = S->isect[(size_t)si];
+    const double n[3] = {T.n[0], T.n[1], T.n[2]};
+    double m = -HUGE_VAL;
+    bool finite = true;
+    for (int a = 0; a < 3; ++a) finite = finite && std::isfinite(n[a]) && std::isfinite(T.c[a]);
+    for (size_t k = 0; k < nv && finite; ++k)
+      m = std::max(m, n[0] * (vx[3 * k] - T.c[0]) + n[1] * (vx[3 * k + 1] - T.c[1]) + n[2] * (vx[3 * k + 2] - T.c[2]));
+    const double tau = (m + h + std::ldexp(r_all, -23) + 1e-9 * r_all) / 1e-2 + 2e-6;
+    for (int a = 0; a < 3; ++a) S->bvh_src_cull[(size_t)si * 4 + a] = T.n[a];
+    S->bvh_src_cull[(size_t)si * 4 + 3] = (finite && nv > 0 && tau < 0.999) ? round_up(tau) : inf;
+  }
+}
+
 bool build_bvh(HostScene *S) {
   S->bvh_nodes.clear();
   S->bvh_pairs.clear();
@@ -754,6 +816,7 @@ bool build_bvh(HostScene *S) {
     S->bvh_big_boxes.clear();
     return false;
   }
+  tree_cull(S, B.prims, r_all);
   S->bvh_status = "ok";
   return true;
 }

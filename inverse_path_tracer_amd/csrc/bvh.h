@@ -19,7 +19,9 @@ bool build_bvh(HostScene *S);
 // hit test of ipt_device.h::hit_test can accept), padded for the rounding of
 // the hit point and of the traversal's slab test.  lo/hi: 3 floats each.
 // Returns 0 = bounded, 1 = never accepted (zero normal), -1 = unbounded.
-int acceptance_box(const TriIsect &T, const TriGeom &G, double r_all, float lo[3], float hi[3]);
+// verts (nullable): the region's six vertices (the prism's two triangles).
+int acceptance_box(const TriIsect &T, const TriGeom &G, double r_all, float lo[3], float hi[3],
+                   double verts[6][3] = nullptr);
 
 // Scene-wide coordinate bound used by the padding (max |vertex coordinate|,
 // |camera origin|, plus one).

@@ -951,6 +951,7 @@ struct CoopView {
   uint32_t *stk;       // LDS: this wave's 8 group stacks, `stride` entries each
   int stride;
   float root[6];       // the tree's box: lo xyz, hi xyz
+  float sphere[4];     // the tree's bounding sphere: centre xyz, padded radius^2 (bvh.cpp tree_cull)
 };
 
 // Whole-wave neighbour shifts (GFX9 DPP wave_shr:1 / wave_shl:1, one VALU
@@ -991,7 +992,15 @@ __device__ __forceinline__ float bperm_f(int addr, float v) {
   return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v)));
 }
 
-// Does the ray reach the tree's box within [0, bt]?
+// Does the ray reach the tree's box within [0, bt], and its bounding sphere?
+// The sphere (bvh.cpp tree_cull: every tree triangle's acceptance region
+// inside, the radius padded far past this test's rounding) drops the rays
+// that cross the box's corners: a ball fills ~half of a box's mean projected
+// area.  A ray whose origin lies outside it and whose line misses it (or
+// points away from it) accepts no tree triangle.
+#ifndef IPT_TREE_SPHERE
+#define IPT_TREE_SPHERE 1
+#endif
 __device__ __forceinline__ bool coop_root_test(const CoopView &C, V3 p, V3 d, float bt) {
   const SlabRay r = slab_ray(p, d);
   const float tx0 = fmaf(C.root[0], r.ix.x, r.ox.x), tx1 = fmaf(C.root[3], r.ix.x, r.ox.x);
@@ -999,7 +1008,25 @@ __device__ __forceinline__ bool coop_root_test(const CoopView &C, V3 p, V3 d, fl
   const float tz0 = fmaf(C.root[2], r.iz.x, r.oz.x), tz1 = fmaf(C.root[5], r.iz.x, r.oz.x);
   const float en = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.f));
   const float ex = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), bt));
+  if (IPT_TREE_SPHERE) {
+    const V3 oc = mk(p.x - C.sphere[0], p.y - C.sphere[1], p.z - C.sphere[2]);
+    const float b = dot3(oc, d), cc = dot3(oc, oc) - C.sphere[3];
+    const bool miss = cc > 0.f && (b > 0.f || fmaf(b, b, -cc) < 0.f);
+    return en <= ex && !miss;
+  }
   return en <= ex;
+}
+// The source-plane test (bvh.cpp tree_cull): the ray leaves a point that
+// triangle s accepted, and dot(n_s, d) >= tau_s puts every tree triangle
+// behind s's plane at every t the hit test accepts.  sc: {n_s, tau_s} per
+// triangle; s < 0 (camera rays): no skip.
+#ifndef IPT_TREE_SKIP
+#define IPT_TREE_SKIP 1
+#endif
+__device__ __forceinline__ bool tree_skip(const float4 *sc, int s, V3 d) {
+  if (s < 0) return false;
+  const float4 v = sc[s];
+  return dot3(mk(v.x, v.y, v.z), d) >= v.w;
 }
 
 // The fp32 test of one triangle without the best-t condition (hit_test's
@@ -1019,6 +1046,102 @@ __device__ __forceinline__ float tri_accept_t(const TriIsect &T, V3 p, V3 d) {
   return ok ? t : __builtin_inff();
 }
 
+// One group's walk of the tree with its ray (gp, gd) from (gt, gi): the 8
+// lanes of the group hold identical copies of the ray state, so every branch
+// is group-uniform.  SHADOW: gi on entry is the target emitter; the walk
+// stops as soon as gi is no longer the target (occluded).
+template <bool SHADOW>
+__device__ __forceinline__ void coop_traverse(const CoopView &C, V3 gp, V3 gd, float &gt, int &gi) {
+  const int lane = (int)__lane_id();
+  const int g = lane >> 3, j = lane & 7;
+  const int target = gi;
+  const SlabRay r = slab_ray(gp, gd);
+  const int oct = (gd.x < 0.f ? 1 : 0) | (gd.y < 0.f ? 2 : 0) | (gd.z < 0.f ? 4 : 0);
+  uint32_t *stk = C.stk + g * C.stride;
+  int node = 0, sp = 0;
+#ifdef IPT_BVH_STATS
+  uint32_t st_nodes = 0, st_leaves = 0;
+#endif
+  for (;;) {
+    if (node >= 0) {  // wide node: lane j tests child j
+#ifdef IPT_BVH_STATS
+      ++st_nodes;
+#endif
+      // lane j tests child j; its rank in the ray octant's front-to-back order
+      float4 a, b;
+      uint32_t rw;
+      if (C.wn_lds) {  // typed per branch: ds_read_b128, not a flat load
+        const lds_f32 *pw = (const lds_f32 *)C.wn + 4 * (2 * (8 * node + oct) + 1) + 3;
+        const lds_v4 *q = (const lds_v4 *)C.wn + 2 * (8 * node + j);
+        rw = __float_as_uint(*pw);
+        const v4f qa = q[0], qb = q[1];
+        a = make_float4(qa.x, qa.y, qa.z, qa.w);
+        b = make_float4(qb.x, qb.y, qb.z, qb.w);
+      } else {
+        const gbl_f32 *pw = (const gbl_f32 *)C.wn + 4 * (2 * (8 * node + oct) + 1) + 3;
+        const gbl_v4 *q = (const gbl_v4 *)C.wn + 2 * (8 * node + j);
+        rw = __float_as_uint(*pw);
+        const v4f qa = q[0], qb = q[1];
+        a = make_float4(qa.x, qa.y, qa.z, qa.w);
+        b = make_float4(qb.x, qb.y, qb.z, qb.w);
+      }
+      const uint32_t rj = (rw >> (3 * j)) & 7u;
+      const int ref = __float_as_int(b.z);
+      const float tx0 = fmaf(a.x, r.ix.x, r.ox.x), tx1 = fmaf(a.w, r.ix.x, r.ox.x);
+      const float ty0 = fmaf(a.y, r.iy.x, r.oy.x), ty1 = fmaf(b.x, r.iy.x, r.oy.x);
+      const float tz0 = fmaf(a.z, r.iz.x, r.oz.x), tz1 = fmaf(b.y, r.iz.x, r.oz.x);
+      const float en = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.f));
+      const float ex = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), gt));
+      const bool h = en <= ex && ref != kWideEmpty;
+      const uint32_t hm = group_or_u32(h ? 1u << rj : 0u);  // hit children by rank
+      if (hm == 0) {
+        node = sp > 0 ? (int)stk[--sp] : kBvhDone;
+      } else {
+        // next = the nearest-ranked hit child; the other hits are pushed
+        // farthest first, so they pop in front-to-back order
+        const uint32_t f = (uint32_t)__builtin_ctz(hm);
+        const int nx = group_min_i32(h && rj == f ? ref : 0x7fffffff);
+        const uint32_t others = hm & (hm - 1u);
+        if ((others >> rj) & 1u) stk[sp + __popc(others >> (rj + 1))] = (uint32_t)ref;
+        sp += __popc(others);
+        node = nx;
+      }
+    } else {  // leaf: lane j tests triangle j (8 per round)
+#ifdef IPT_BVH_STATS
+      ++st_leaves;
+#endif
+      const int code = ~node;
+      const int first = code >> 4, cnt = (code & 15) + 1;
+#ifdef IPT_BVH_STATS
+      if (j == 0) atomicAdd(&g_bvh_stats[4], (unsigned long long)cnt);
+#endif
+      for (int base = 0; base < cnt; base += 8) {
+        float tj = __builtin_inff();
+        int ij = 0x7fffffff;
+        if (base + j < cnt) {
+          const TriIsect &T = C.wt[first + base + j];
+          tj = tri_accept_t(T, gp, gd);
+          ij = __float_as_int(T.pad[0]);
+        }
+        group_lexmin(tj, ij);
+        const bool take = (tj < gt) | ((tj == gt) & (ij < gi));
+        gt = take ? tj : gt;
+        gi = take ? ij : gi;
+      }
+      node = (SHADOW && gi != target) ? kBvhDone : (sp > 0 ? (int)stk[--sp] : kBvhDone);
+    }
+    if (node == kBvhDone) break;
+  }
+#ifdef IPT_BVH_STATS
+  if (j == 0) {
+    atomicAdd(&g_bvh_stats[0], 1ull);
+    atomicAdd(&g_bvh_stats[1], (unsigned long long)st_nodes);
+    atomicAdd(&g_bvh_stats[2], (unsigned long long)st_leaves);
+    if (SHADOW && gi != target) atomicAdd(&g_bvh_stats[3], 1ull);
+  }
+#endif
+}
+
 // Cooperative closest hit.  Called by ALL 64 lanes of the wave (convergent);
 // lanes with `need` have their (bt, bi) continued through the tree
 // lexicographically.  SHADOW: the lanes' entry bi is the target emitter; a
@@ -1026,7 +1149,7 @@ __device__ __forceinline__ float tri_accept_t(const TriIsect &T, V3 p, V3 d) {
 template <bool SHADOW>
 __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3 d, float &bt, int &bi) {
   const int lane = (int)__lane_id();
-  const int g = lane >> 3, j = lane & 7;
+  const int g = lane >> 3;
   uint64_t M = __ballot(need);
 #ifdef IPT_BVH_STATS
   if (M && lane == (int)__builtin_ctzll(__ballot(1))) atomicAdd(&g_bvh_stats[5], 1ull);
@@ -1053,92 +1176,7 @@ __device__ __forceinline__ void coop_cast(const CoopView &C, bool need, V3 p, V3
     float gt = bperm_f(sa, bt);
     int gi = __builtin_amdgcn_ds_bpermute(sa, bi);
     if (src >= 0) {
-      const int target = gi;
-      const SlabRay r = slab_ray(gp, gd);
-      const int oct = (gd.x < 0.f ? 1 : 0) | (gd.y < 0.f ? 2 : 0) | (gd.z < 0.f ? 4 : 0);
-      uint32_t *stk = C.stk + g * C.stride;
-      int node = 0, sp = 0;
-#ifdef IPT_BVH_STATS
-      uint32_t st_nodes = 0, st_leaves = 0;
-#endif
-      for (;;) {
-        if (node >= 0) {  // wide node: lane j tests child j
-#ifdef IPT_BVH_STATS
-          ++st_nodes;
-#endif
-          // lane j tests child j; its rank in the ray octant's front-to-back order
-          float4 a, b;
-          uint32_t rw;
-          if (C.wn_lds) {  // typed per branch: ds_read_b128, not a flat load
-            const lds_f32 *pw = (const lds_f32 *)C.wn + 4 * (2 * (8 * node + oct) + 1) + 3;
-            const lds_v4 *q = (const lds_v4 *)C.wn + 2 * (8 * node + j);
-            rw = __float_as_uint(*pw);
-            const v4f qa = q[0], qb = q[1];
-            a = make_float4(qa.x, qa.y, qa.z, qa.w);
-            b = make_float4(qb.x, qb.y, qb.z, qb.w);
-          } else {
-            const gbl_f32 *pw = (const gbl_f32 *)C.wn + 4 * (2 * (8 * node + oct) + 1) + 3;
-            const gbl_v4 *q = (const gbl_v4 *)C.wn + 2 * (8 * node + j);
-            rw = __float_as_uint(*pw);
-            const v4f qa = q[0], qb = q[1];
-            a = make_float4(qa.x, qa.y, qa.z, qa.w);
-            b = make_float4(qb.x, qb.y, qb.z, qb.w);
-          }
-          const uint32_t rj = (rw >> (3 * j)) & 7u;
-          const int ref = __float_as_int(b.z);
-          const float tx0 = fmaf(a.x, r.ix.x, r.ox.x), tx1 = fmaf(a.w, r.ix.x, r.ox.x);
-          const float ty0 = fmaf(a.y, r.iy.x, r.oy.x), ty1 = fmaf(b.x, r.iy.x, r.oy.x);
-          const float tz0 = fmaf(a.z, r.iz.x, r.oz.x), tz1 = fmaf(b.y, r.iz.x, r.oz.x);
-          const float en = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.f));
-          const float ex = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), gt));
-          const bool h = en <= ex && ref != kWideEmpty;
-          const uint32_t hm = group_or_u32(h ? 1u << rj : 0u);  // hit children by rank
-          if (hm == 0) {
-            node = sp > 0 ? (int)stk[--sp] : kBvhDone;
-          } else {
-            // next = the nearest-ranked hit child; the other hits are pushed
-            // farthest first, so they pop in front-to-back order
-            const uint32_t f = (uint32_t)__builtin_ctz(hm);
-            const int nx = group_min_i32(h && rj == f ? ref : 0x7fffffff);
-            const uint32_t others = hm & (hm - 1u);
-            if ((others >> rj) & 1u) stk[sp + __popc(others >> (rj + 1))] = (uint32_t)ref;
-            sp += __popc(others);
-            node = nx;
-          }
-        } else {  // leaf: lane j tests triangle j (8 per round)
-#ifdef IPT_BVH_STATS
-          ++st_leaves;
-#endif
-          const int code = ~node;
-          const int first = code >> 4, cnt = (code & 15) + 1;
-#ifdef IPT_BVH_STATS
-          if (j == 0) atomicAdd(&g_bvh_stats[4], (unsigned long long)cnt);
-#endif
-          for (int base = 0; base < cnt; base += 8) {
-            float tj = __builtin_inff();
-            int ij = 0x7fffffff;
-            if (base + j < cnt) {
-              const TriIsect &T = C.wt[first + base + j];
-              tj = tri_accept_t(T, gp, gd);
-              ij = __float_as_int(T.pad[0]);
-            }
-            group_lexmin(tj, ij);
-            const bool take = (tj < gt) | ((tj == gt) & (ij < gi));
-            gt = take ? tj : gt;
-            gi = take ? ij : gi;
-          }
-          node = (SHADOW && gi != target) ? kBvhDone : (sp > 0 ? (int)stk[--sp] : kBvhDone);
-        }
-        if (node == kBvhDone) break;
-      }
-#ifdef IPT_BVH_STATS
-      if (j == 0) {
-        atomicAdd(&g_bvh_stats[0], 1ull);
-        atomicAdd(&g_bvh_stats[1], (unsigned long long)st_nodes);
-        atomicAdd(&g_bvh_stats[2], (unsigned long long)st_leaves);
-        if (SHADOW && gi != target) atomicAdd(&g_bvh_stats[3], 1ull);
-      }
-#endif
+      coop_traverse<SHADOW>(C, gp, gd, gt, gi);
     }
     // results back to the owners: the ray of group k came from the k-th lane of `taken`
     const int ra = (8 * lane_rank64(taken)) << 2;

@@ -229,6 +229,8 @@ struct TraceArgs {
   int bvh_wide_lds, coop_stride;
   int bvh_big_lds;  // culled path pre-pass: the large pairs' LDS copy is built (launch_bvh chooses)
   float root_box[6];
+  float tree_sphere[4];     // bvh.cpp tree_cull
+  const float4 *src_cull;   // per triangle {face normal, tau} (ipt_device.h tree_skip)
   const TriPair *bvh_big;
   const int32_t *bvh_big_idx;
   const PairBox2 *bvh_big_boxes;
@@ -501,7 +503,12 @@ constexpr int min_blocks() {
 // (r03/variants_queue_chsweep_r03f.log: north-star forward 4.70 vs 3.75 ms;
 // r03/variants_r03e.log for the first form, 4.30 ms) and a channel-split
 // adjoint sweep, lane 3i + c walking path i in channel c (same log: C2
-// adjoint 2.33 vs 2.16 ms, north-star 6.57 vs 5.02 ms at one wave less).
+// adjoint 2.33 vs 2.16 ms, north-star 6.57 vs 5.02 ms at one wave less);
+// round 5: the four waves of a workgroup pooling their tree rays in an LDS
+// queue and sharing out full rounds of 8 (two barriers per cast, the waves in
+// step): north-star forward 3.71 -> 4.25 ms, unbounded adjoint 8.06 -> 13.6 --
+// the lockstep waits cost more than the fuller rounds save
+// (profiles/r05/variants_coop_wg_r05i.log, _r05j.log).
 // Graph bins stay in LDS up to this size (KB), else global fp64 atomics.
 #ifndef IPT_GRAPH_LDS_KB
 #define IPT_GRAPH_LDS_KB 64
@@ -753,6 +760,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   cv.stk = nullptr;
   cv.stride = a.coop_stride;
   for (int k = 0; k < 6; ++k) cv.root[k] = a.root_box[k];
+  for (int k = 0; k < 4; ++k) cv.sphere[k] = a.tree_sphere[k];
   if (BVH) {
     const size_t rec_words = is_badj<MODE>()    ? (size_t)vmax * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock
                              : MODE == MODE_ADJU ? (size_t)a.rec_lds * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse) * kBlock
@@ -872,6 +880,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   float weight = 1.f;  // GRAPH path weight
   V3 pix = p;          // GRAPH target pixel
   int k = 0, dst = 0;
+  int ptri = -1;       // BVH: the triangle the path ray leaves (tree_skip), -1 = camera ray
   uint64_t witem = 0;  // this lane's work item (output slot / pixel source)
   // One iteration = one path vertex for the whole wave, in two
   // wave-synchronous phases: (1) every active lane casts its path ray and,
@@ -1039,6 +1048,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           Ld = L;
           M = mk(1.f, 1.f, 1.f);
           k = 0;
+          ptri = -1;
           active = true;
         }
         fj += (uint32_t)__popcll(need);
@@ -1058,6 +1068,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           Ld = L;
           M = mk(1.f, 1.f, 1.f);
           k = 0;
+          ptri = -1;
           if (MODE == MODE_ADJU) {
             rhi = 0;
             rslot = 0;
@@ -1090,7 +1101,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       bool qn = false;
       if (active) {
         bvh_prepass<false>(bv, p, d, t, hit, -1);
-        qn = coop_root_test(cv, p, d, t);
+        qn = coop_root_test(cv, p, d, t) && !(IPT_TREE_SKIP && tree_skip(a.src_cull, ptri, d));
       }
       SUBPHASE_BEGIN
       coop_cast<false>(cv, qn, p, d, t, hit);
@@ -1198,7 +1209,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         bool qn = false;
         if (shadow && bvh_prepass<true>(bv, p, sd, ts, hs, et,
                                         a.big_pomask ? a.big_pomask[tri * nE + emitter] : 0xffffffffu, emitter))
-          qn = coop_root_test(cv, p, sd, ts);
+          qn = coop_root_test(cv, p, sd, ts) && !(IPT_TREE_SKIP && tree_skip(a.src_cull, tri, sd));
         SUBPHASE_BEGIN
         coop_cast<true>(cv, qn, p, sd, ts, hs);
         SUBPHASE_END(9)
@@ -1321,6 +1332,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         }
       }
       ++k;  // vertices so far
+      if (BVH) ptri = tri;
       if (cont) d = nd;
       else finished = true;
       if (MODE == MODE_ADJU && rhi > 0 && k == rhi) finished = true;  // replay reached its target
@@ -1597,6 +1609,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         M = mk(1.f, 1.f, 1.f);
         Mlo = M;
         k = 0;
+        ptri = -1;
         rslot = 0;
         rhi = urep;
         active = true;
@@ -1746,6 +1759,7 @@ struct GpuScene {
   int32_t *big_idx = nullptr;
   PairBox2 *big_boxes = nullptr;
   float4 *wide = nullptr;  // WideNode records
+  float4 *src_cull = nullptr;  // HostScene::bvh_src_cull
   TriIsect *wtris = nullptr;
   PairBox2 *pboxes = nullptr;  // pair acceptance boxes (small scenes' culled shadow casts)
   uint32_t *pomask = nullptr;  // shadow rays' potential occluders (small scenes)
@@ -1807,6 +1821,14 @@ static int upload_as_f4(float4 **dst, const std::vector<T> &v) {
   return 0;
 }
 
+static std::vector<float4> src_cull_f4(const HostScene &host) {
+  std::vector<float4> v(host.bvh_src_cull.size() / 4);
+  for (size_t i = 0; i < v.size(); ++i)
+    v[i] = make_float4(host.bvh_src_cull[4 * i], host.bvh_src_cull[4 * i + 1], host.bvh_src_cull[4 * i + 2],
+                       host.bvh_src_cull[4 * i + 3]);
+  return v;
+}
+
 GpuScene *gpu_upload(const HostScene &host, std::string *err) {
   GpuScene *s = new GpuScene();
   s->host = host;
@@ -1822,7 +1844,7 @@ GpuScene *gpu_upload(const HostScene &host, std::string *err) {
       upload(&s->emit_pmf, host.emit_pmf) || upload(&s->emit_pmfr, pmf_reciprocals(host.emit_pmf)) ||
       upload(&s->big_pairs, host.bvh_big_pairs) || upload(&s->big_idx, host.bvh_big_idx) ||
       upload(&s->big_boxes, host.bvh_big_boxes) ||
-      upload_as_f4(&s->wide, host.bvh_wide) ||
+      upload_as_f4(&s->wide, host.bvh_wide) || upload(&s->src_cull, src_cull_f4(host)) ||
       upload(&s->wtris, host.bvh_wtris) || upload(&s->pboxes, pair_boxes(host)) ||
       upload(&s->pomask, shadow_occluder_masks(host)) ||
       upload(&s->big_pomask, host.bvh_big_idx.empty()
@@ -1889,6 +1911,7 @@ void gpu_free(GpuScene *s) {
   (void)hipFree(s->big_idx);
   (void)hipFree(s->big_boxes);
   (void)hipFree(s->wide);
+  (void)hipFree(s->src_cull);
   (void)hipFree(s->wtris);
   (void)hipFree(s->pboxes);
   (void)hipFree(s->pomask);
@@ -2006,6 +2029,8 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.bvh_big_lds = 0;
   a.coop_stride = 0;
   for (int k = 0; k < 6; ++k) a.root_box[k] = s->host.bvh_root_box[k];
+  for (int k = 0; k < 4; ++k) a.tree_sphere[k] = s->host.bvh_sphere[k];
+  a.src_cull = s->src_cull;
   a.grad_slots = 0;
   a.grad_map = nullptr;
   a.slot_tri = nullptr;
@@ -2772,6 +2797,7 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
   cv.stk = nullptr;
   cv.stride = a.coop_stride;
   for (int k = 0; k < 6; ++k) cv.root[k] = a.root_box[k];
+  for (int k = 0; k < 4; ++k) cv.sphere[k] = a.tree_sphere[k];
   if (BVH) {
     char *base = reinterpret_cast<char *>(lds);
     float4 *lw = reinterpret_cast<float4 *>(base + bvh_lds_offset((size_t)(small ? kE3Floats * nP : 0) * sizeof(float)));
@@ -2804,6 +2830,7 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
     d = mk(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);
     target = targets ? targets[i] : -1;
     src = sources ? sources[i] : -1;
+    src = src < nT ? src : -1;
   }
   float t = 0.f;
   int h = -1;
@@ -2812,10 +2839,11 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
     if (valid) {
       if (target >= 0) {
         const uint32_t allow = probe_allow(IPT_SHADOW_PO ? a.big_pomask : nullptr, emit_tri, a.nE, nT, src, target);
-        if (bvh_prepass<true>(bv, p, d, t, h, target, allow)) qn = coop_root_test(cv, p, d, t);
-      } else {
+        if (bvh_prepass<true>(bv, p, d, t, h, target, allow))
+          qn = coop_root_test(cv, p, d, t) && !(IPT_TREE_SKIP && tree_skip(a.src_cull, src, d));
+      } else {  // (a path ray with a source: the megakernel's bounce ray leaving that triangle)
         bvh_prepass<false>(bv, p, d, t, h, -1);
-        qn = coop_root_test(cv, p, d, t);
+        qn = coop_root_test(cv, p, d, t) && !(IPT_TREE_SKIP && tree_skip(a.src_cull, src, d));
       }
     }
     coop_cast<false>(cv, qn && target < 0, p, d, t, h);

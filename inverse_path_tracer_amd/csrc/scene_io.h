@@ -42,6 +42,10 @@ struct HostScene {
   std::vector<TriIsect> bvh_wtris;  // leaf triangles (pad[0] = original index)
   int bvh_wdepth = 0;               // wide levels
   float bvh_root_box[6] = {0, 0, 0, 0, 0, 0};  // lo xyz, hi xyz of the whole tree
+  // tree entry tests (bvh.cpp tree_cull): bounding sphere (centre xyz,
+  // padded radius^2) and per source triangle {face normal xyz, tau}
+  float bvh_sphere[4] = {0, 0, 0, 0};
+  std::vector<float> bvh_src_cull;
   std::string bvh_status;      // "ok" or why the BVH was not built
 };
 

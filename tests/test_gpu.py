@@ -806,6 +806,79 @@ def test_culled_path_cast_equals_brute_force(oracle, which):
     P.close()
 
 
+@pytest.mark.parametrize("which", ["northstar", "clutter"])
+def test_tree_entry_culls_equal_brute_force(which):
+    """BVH scenes: the tree's entry tests (bvh.cpp tree_cull) -- the bounding
+    sphere of its triangles' acceptance regions and the source-plane skip of
+    rays leaving a triangle with every tree triangle behind its plane (the
+    sphere's own faces) -- return the full brute-force loop's hit bit-for-bit:
+    bounce rays (targets -1) from points on every triangle, in all
+    directions, grazing ones within 1e-3 of the plane and a fifth near the
+    skip's threshold; rays from the room towards points just outside and
+    inside the tree's bounding sphere; shadow rays with their source."""
+    from inverse_path_tracer_amd import _native as N
+    from conftest import NORTHSTAR
+    from test_bvh import CLUTTER_SCENE, _shadow_rays
+
+    P = product_scene(NORTHSTAR if which == "northstar" else CLUTTER_SCENE)
+    assert P.bvh_info()["accel"] == "bvh"
+    tris = P.triangles()
+    v = tris[:, 0:9].reshape(-1, 3, 3).astype(np.float64)
+    rng = np.random.RandomState(41)
+    n = 300000
+    src = rng.randint(0, P.nT, n)
+    a, b = rng.uniform(0, 1, (2, n))
+    flip = a + b > 1
+    a[flip], b[flip] = 1 - a[flip], 1 - b[flip]
+    O = v[src, 0] + a[:, None] * (v[src, 1] - v[src, 0]) + b[:, None] * (v[src, 2] - v[src, 0])
+    nrm = np.cross(v[src, 1] - v[src, 0], v[src, 2] - v[src, 0])
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    D = rng.normal(size=(n, 3))
+    D /= np.linalg.norm(D, axis=1, keepdims=True)
+    kind = rng.uniform(0, 1, n)
+    graze = kind < 0.25  # within ~1e-3 of the plane, either side
+    Dg = D - np.sum(D * nrm, 1)[:, None] * nrm
+    D[graze] = Dg[graze] + rng.normal(0, 1e-3, (int(graze.sum()), 3))
+    near = (kind >= 0.25) & (kind < 0.45)  # cos to the face normal near the skip's threshold (~0.02-0.05)
+    c = rng.uniform(0.0, 0.08, int(near.sum()))
+    Dt = Dg[near] / np.maximum(np.linalg.norm(Dg[near], axis=1, keepdims=True), 1e-30)
+    D[near] = Dt * np.sqrt(1 - c * c)[:, None] + nrm[near] * c[:, None]
+    D /= np.linalg.norm(D, axis=1, keepdims=True)
+    # rays from the room aimed at points on and just off the objects (not the
+    # Cornell box's 18 triangles): silhouettes and the bounding sphere's rim
+    m = 100000
+    box = v.reshape(-1, 3)
+    Or = rng.uniform(box.min(0), box.max(0), (m, 3))
+    k = rng.randint(18, P.nT, m)
+    a2, b2 = rng.uniform(0, 1, (2, m))
+    flip = a2 + b2 > 1
+    a2[flip], b2[flip] = 1 - a2[flip], 1 - b2[flip]
+    aim = v[k, 0] + a2[:, None] * (v[k, 1] - v[k, 0]) + b2[:, None] * (v[k, 2] - v[k, 0])
+    aim += rng.normal(0, 0.03, (m, 3))
+    Dr = aim - Or
+    Dr /= np.linalg.norm(Dr, axis=1, keepdims=True)
+    O = np.concatenate([O, Or]).astype(np.float32)
+    D = np.concatenate([D, Dr]).astype(np.float32)
+    S = np.concatenate([src, np.full(m, -1)]).astype(np.int32)
+    tg = np.full(len(O), -1, np.int32)
+    tc, ic = P.shadow_hit(O, D, tg, S)  # the megakernel's BVH path cast with the source triangle
+    P.set_accel(N.ACCEL_BRUTE)
+    tf, i_f = P.closest_hit(O, D)
+    P.set_accel(N.ACCEL_AUTO)
+    assert np.array_equal(ic, i_f)
+    assert np.array_equal(bits(tc), bits(tf))
+    # shadow rays with their source triangle (the sphere's faces towards the light included)
+    Os, Ds, tgs, srcs, _, _ = _shadow_rays(tris, 300000, np.random.RandomState(43))
+    tc, ic = P.shadow_hit(Os, Ds, tgs, srcs)
+    P.set_accel(N.ACCEL_BRUTE)
+    tf, i_f = P.closest_hit(Os, Ds)
+    P.set_accel(N.ACCEL_AUTO)
+    vis_c, vis_f = ic == tgs, i_f == tgs
+    assert np.array_equal(vis_c, vis_f)
+    assert np.array_equal(bits(tc[vis_c]), bits(tf[vis_f]))
+    P.close()
+
+
 @pytest.mark.parametrize("which", ["cornell", "scene0", "northstar"])
 def test_masked_shadow_query_equals_brute_force(which):
     """The megakernel's shadow cast with the static potential-occluder mask of

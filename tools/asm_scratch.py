@@ -12,7 +12,7 @@ def main():
     path, mode, spec, bvh = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4]
     s = open(path).read().split("\n")
     tag = "_ZN3ipt12trace_kernelILi%sELb%sELb%sE" % (mode, spec, bvh)
-    i = next(k for k, l in enumerate(s) if l.startswith(tag) and l.split(":")[0].endswith("SP_"))
+    i = next(k for k, l in enumerate(s) if l.startswith(tag) and re.match(re.escape(tag) + r"\S*:", l))
     j = i
     while "s_endpgm" not in s[j]:
         j += 1
