@@ -53,6 +53,10 @@ CUBE = ObjectSpec(os.path.join(ASSETS, "shapes", "cube.obj"),
                   "*Kd 0.9041462985304743 0.5854651848798454 0.007022117649276849*", (0, -1.5, 4), (0, 0, 0),
                   (1, 1, 1))
 SCENE0 = CORNELL + [CUBE]
+# scenes/0.txt with the cube given a Phong lobe (Ks 0.5, shininess 20; assets/phong/scene0_phong.txt):
+# the reference's BSDF supports Ks != 0 (path_trace.cu:10-28, 91-109); the SPEC kernel instances run it
+SCENE0_PHONG = CORNELL + [ObjectSpec(os.path.join(ASSETS, "phong", "cube_phong.obj"),
+                                     os.path.join(ASSETS, "phong", "cube_phong.mtl"), (0, -1.5, 4), (0, 0, 0), (1, 1, 1))]
 # BASELINE configs[2] as the north_star names it: scenes/0.txt + sphere.obj (assets/northstar.txt), 1310 triangles
 NORTHSTAR = SCENE0 + [ObjectSpec(os.path.join(ASSETS, "shapes", "sphere.obj"), "*Kd 0.2 0.6 0.3*", (-1.2, -1.35, 4.6),
                                  (0.0, 0.0, 0.0), (1.2, 1.2, 1.2))]
@@ -73,6 +77,7 @@ PMC_FILE = os.path.join(ROOT, "profiles", "pmc_fwd_trace_kernel.json")
 # (tools/bvh_stats.py -> profiles/bvh_stats.json: 38 per triangle test + 12
 # per slab test)
 CASTS_PER_SAMPLE_C3 = 5.61259913444519
+CASTS_PER_SAMPLE_PHONG = 5.586296021938324  # C3 with the Phong cube (tools/count_casts.py C3_phong_512x512x64_b4)
 # createGraph's integrator at the reference's configuration (scenes/0.txt,
 # 500x500, 100 spp, no bounce cap): tools/count_casts.py with the oracle
 CASTS_PER_SAMPLE_GRAPH = 7.1221316
@@ -103,6 +108,8 @@ def executed_flop_per_sample(name, c_bar, n_tri):
 def flop_per_sample(key):
     if key == "c3":
         return CASTS_PER_SAMPLE_C3 * 30 * FLOP_PER_TEST, "C_bar(C3) * 30 * 38"
+    if key == "c3_phong":
+        return CASTS_PER_SAMPLE_PHONG * 30 * FLOP_PER_TEST, "C_bar(C3 Phong cube) * 30 * 38"
     name = {"c3_northstar": "northstar", "bvh_sphere": "sphere"}.get(key)
     if name and os.path.exists(BVH_STATS_FILE):
         with open(BVH_STATS_FILE) as f:
@@ -468,6 +475,8 @@ def main():
         # other configurations, this rank's band of an N-way tile split
         for key, objs, w, h, spp, mb, desc in (
                 ("c3", SCENE0, W, H, SPP, BOUNCES, "C3: scenes/0.txt (Cornell + cube, 30 triangles), 512x512, 64 spp, 4 bounces"),
+                ("c3_phong", SCENE0_PHONG, W, H, SPP, BOUNCES, "C3 with a Phong cube (Ks 0.5, shininess 20; "
+                 "assets/phong/scene0_phong.txt): the SPEC kernel instances, 512x512, 64 spp, 4 bounces"),
                 ("c3_unbounded", SCENE0, W, H, SPP, None, "C3 with the reference's own estimator (no bounce cap: "
                  "Russian roulette only), scenes/0.txt, 512x512, 64 spp; fused render (slot ring); adjoint = global "
                  "record ring + chunk replay"),

@@ -223,7 +223,13 @@ __device__ inline double exp_d(double x) {
   const double s2 = __longlong_as_double((long long)((uint64_t)(k2 + 1023) << 52));
   return (p * s1) * s2;
 }
-__device__ inline double pow_d(double x, double y) {
+// Out of line: the megakernel's SPEC instances (materials with a Phong lobe)
+// call it from the sampling and BSDF code.  Inlined, its ~35 polynomial
+// constants were hoisted out of the trace loop into registers, and every
+// SPEC instance spilled 164-292 B per lane inside the loop even on diffuse
+// vertices; as a call, the constants live in the callee and the caller saves
+// registers only around the (Phong-only) call.
+__device__ __attribute__((noinline)) double pow_d(double x, double y) {
   if (y == 0.0) return 1.0;
   if (x == 0.0) return y > 0 ? 0.0 : __builtin_inf();
   return exp_d(y * log_d(x));

@@ -31,6 +31,9 @@ if os.environ.get("IPT_VB_CLUTTER"):  # the 4-object scene of tests/test_bvh.py 
 if os.environ.get("IPT_VB_NORTHSTAR"):  # BASELINE configs[2]: scenes/0.txt + sphere (1310 triangles)
     SCENES["northstar"] = SCENES["scene0"] + [(A + "/shapes/sphere.obj", "*Kd 0.2 0.6 0.3*", (-1.2, -1.35, 4.6),
                                                (0.0, 0.0, 0.0), (1.2, 1.2, 1.2))]
+if os.environ.get("IPT_VB_PHONG"):  # scenes/0.txt with a Phong cube (bench.py c3_phong): the SPEC instances
+    SCENES["phong"] = SCENES["cornell"] + [(A + "/phong/cube_phong.obj", A + "/phong/cube_phong.mtl", (0, -1.5, 4),
+                                            (0, 0, 0), (1, 1, 1))]
 if os.environ.get("IPT_VB_ONLY"):  # comma-separated scene names
     SCENES = {k: v for k, v in SCENES.items() if k in os.environ["IPT_VB_ONLY"].split(",")}
 
