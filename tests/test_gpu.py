@@ -96,6 +96,30 @@ def test_specular_material_bit_exact(oracle, tmp_path):
     np.testing.assert_allclose(P.adjoint(adj, 32, 32, 8, 4, 4), Q.adjoint(32, 32, 8, 4, 4, adj), rtol=1e-9, atol=1e-12)
 
 
+def test_phong_scene_fused_render_and_unbounded_adjoint(oracle):
+    """The bench's c3_phong scene (assets/phong: the cube with Ks 0.5,
+    shininess 20) through the SPEC instances the other Phong test does not
+    reach: the fused render (HDR = the oracle's toneMap, bitwise, bounded and
+    unbounded paths) and the unbounded adjoint (rtol 1e-9)."""
+    import oracle_lib
+    from conftest import ASSETS
+
+    recs = CORNELL + [((0, -1.5, 4), (0, 0, 0), (1, 1, 1), os.path.join(ASSETS, "phong", "cube_phong.obj"),
+                       os.path.join(ASSETS, "phong", "cube_phong.mtl"))]
+    P, Q = product_scene(recs), oracle.OracleScene(recs)
+    assert np.any(P.triangles()[:, 28:31] > 0)
+    W, H, spp, seed = 40, 24, 16, 6
+    for mb in (4, None):
+        hdr = P.render(W, H, spp, mb, seed)
+        s, _ = Q.render_samples(W, H, spp, mb, seed)
+        hq, _ = oracle_lib.pixel_mean(s, W * H, spp)
+        assert np.array_equal(bits(hdr.reshape(-1, 3)), bits(hq)), mb
+    adj = np.random.RandomState(1).uniform(-1, 1, (H, W, 3)).astype(np.float32)
+    np.testing.assert_allclose(P.adjoint(adj, W, H, spp, None, seed), Q.adjoint(W, H, spp, None, seed, adj),
+                               rtol=1e-9, atol=1e-12)
+    P.close()
+
+
 def test_no_emitters_is_black_not_nan(oracle):
     recs = [((0, -1.5, 4), (0, 0, 0), (1, 1, 1), CUBE_OBJ, "*Kd 0.5 0.5 0.5*")]
     P, Q = product_scene(recs), oracle.OracleScene(recs)
