@@ -153,11 +153,13 @@ int ipt_closest_hit_host(void *scene, int64_t n, const float *origins, const flo
                          float *t, int32_t *idx);
 int ipt_closest_hit_dev(void *scene, int64_t n, const float *origins_dev, const float *dirs_dev,
                         const int32_t *targets_dev, float *t_dev, int32_t *idx_dev, void *stream);
-/* Shadow rays exactly as the megakernel casts them from a path vertex:
- * sources[i] >= 0 is the triangle the origin lies on (its vertex), which in
- * small scenes selects the static potential-occluder mask of (source,
- * emitter) on top of the culled shadow cast; < 0 = no mask.  targets[i] >= 0
- * as in ipt_closest_hit_host (both arrays required). */
+/* Rays exactly as the megakernel casts them from a path vertex:
+ * sources[i] >= 0 is the triangle the origin lies on (a point its hit test
+ * accepted), which selects the static potential-occluder mask of (source,
+ * emitter) on top of the culled shadow cast, and in BVH scenes the tree's
+ * source-plane skip; < 0 = none.  targets[i] >= 0 = a shadow ray towards that
+ * emitter, < 0 = a bounce ray (the path cast), as in ipt_closest_hit_host
+ * (both arrays required). */
 int ipt_shadow_hit_host(void *scene, int64_t n, const float *origins, const float *dirs, const int32_t *targets,
                         const int32_t *sources, float *t, int32_t *idx);
 

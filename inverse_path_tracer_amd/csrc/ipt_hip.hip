@@ -753,6 +753,13 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   bv.big_boxes = nullptr;
   bv.big_lds = nullptr;
   bv.emit_is = nullptr;
+  // BVH forward (5 waves/SIMD, 96 VGPRs): the lane's work item, the triangle
+  // its path ray leaves and its first emission Le live in LDS ([6][kBlock]
+  // words: item lo, hi, source, Le xyz) instead of registers -- each is
+  // touched a few times per path, and in registers the allocator spilled them
+  // (and more) to scratch inside the loop
+  constexpr bool kLaneLds = BVH && is_fwd<MODE>();
+  lds_u32 *lane_ws = nullptr;
   CoopView cv;
   cv.wn = nullptr;
   cv.wn_lds = false;
@@ -791,6 +798,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       after += 20 * nE;
     }
     cv.stk = reinterpret_cast<uint32_t *>(after) + (tid >> 6) * 8 * a.coop_stride;
+    if (kLaneLds) lane_ws = (lds_u32 *)(reinterpret_cast<uint32_t *>(after) + (kBlock / 64) * 8 * a.coop_stride);
   }
   for (int i = tid; i < n_acc; i += nthr) lds_acc[i] = 0.0;
   __syncthreads();
@@ -870,7 +878,23 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   bool active = false;
   Rng st;
   V3 p = mk(0.f, 0.f, 0.f), d = p;
-  V3 L = p, Le = p, Ld = p, M = mk(1.f, 1.f, 1.f);
+  V3 L = p, Le_r = p, Ld = p, M = mk(1.f, 1.f, 1.f);
+  // Le: the path's first emission (kLaneLds: in LDS words 3..5 of lane_ws)
+  auto set_le = [&](V3 v) {
+    if (kLaneLds) {
+      ((lds_f32 *)lane_ws)[3 * kBlock + tid] = v.x;
+      ((lds_f32 *)lane_ws)[4 * kBlock + tid] = v.y;
+      ((lds_f32 *)lane_ws)[5 * kBlock + tid] = v.z;
+    } else {
+      Le_r = v;
+    }
+  };
+  auto le = [&]() -> V3 {
+    if (kLaneLds)
+      return mk(((lds_f32 *)lane_ws)[3 * kBlock + tid], ((lds_f32 *)lane_ws)[4 * kBlock + tid],
+                ((lds_f32 *)lane_ws)[5 * kBlock + tid]);
+    return Le_r;
+  };
   // ADJU (unbounded adjoint): suffix carried from the chunk after, replay
   // target (0 = first pass), next ring slot
   // and the prefix throughput at the chunk's first vertex (1 for a chunk
@@ -880,8 +904,25 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   float weight = 1.f;  // GRAPH path weight
   V3 pix = p;          // GRAPH target pixel
   int k = 0, dst = 0;
-  int ptri = -1;       // BVH: the triangle the path ray leaves (tree_skip), -1 = camera ray
-  uint64_t witem = 0;  // this lane's work item (output slot / pixel source)
+  int ptri_r = -1;       // BVH: the triangle the path ray leaves (tree_skip), -1 = camera ray
+  uint64_t witem_r = 0;  // this lane's work item (output slot / pixel source)
+  auto set_item = [&](uint64_t w) {
+    if (kLaneLds) {
+      lane_ws[tid] = (uint32_t)w;
+      lane_ws[kBlock + tid] = (uint32_t)(w >> 32);
+    } else {
+      witem_r = w;
+    }
+  };
+  auto witem = [&]() -> uint64_t {
+    if (kLaneLds) return (uint64_t)lane_ws[tid] | ((uint64_t)lane_ws[kBlock + tid] << 32);
+    return witem_r;
+  };
+  auto set_ptri = [&](int t) {
+    if (kLaneLds) lane_ws[2 * kBlock + tid] = (uint32_t)t;
+    else ptri_r = t;
+  };
+  auto ptri = [&]() -> int { return kLaneLds ? (int)lane_ws[2 * kBlock + tid] : ptri_r; };
   // One iteration = one path vertex for the whole wave, in two
   // wave-synchronous phases: (1) every active lane casts its path ray and,
   // on a hit, shades the vertex and draws ALL of the vertex's random numbers
@@ -1042,13 +1083,13 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           int r, c;
           item_ray_ls(a, seed, glp + q, s, st, p, d, r, c);
           // the sample's LDS place: its pixel's slot, sample s
-          witem = (uint64_t)((gslots >> (4 * q)) & 15u) | ((uint64_t)s << 4);
+          set_item((uint64_t)((gslots >> (4 * q)) & 15u) | ((uint64_t)s << 4));
           L = mk(0.f, 0.f, 0.f);
-          Le = L;
+          set_le(L);
           Ld = L;
           M = mk(1.f, 1.f, 1.f);
           k = 0;
-          ptri = -1;
+          set_ptri(-1);
           active = true;
         }
         fj += (uint32_t)__popcll(need);
@@ -1060,15 +1101,15 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       if (!active) {
         const uint64_t w = next + rank;
         if (w < end) {
-          witem = w;
+          set_item(w);
           int r, c;
           item_ray(a, seed, w, st, p, d, r, c);
           L = mk(0.f, 0.f, 0.f);
-          Le = L;
+          set_le(L);
           Ld = L;
           M = mk(1.f, 1.f, 1.f);
           k = 0;
-          ptri = -1;
+          set_ptri(-1);
           if (MODE == MODE_ADJU) {
             rhi = 0;
             rslot = 0;
@@ -1101,7 +1142,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       bool qn = false;
       if (active) {
         bvh_prepass<false>(bv, p, d, t, hit, -1);
-        qn = coop_root_test(cv, p, d, t) && !(IPT_TREE_SKIP && tree_skip(a.src_cull, ptri, d));
+        qn = coop_root_test(cv, p, d, t) && !(IPT_TREE_SKIP && tree_skip(a.src_cull, ptri(), d));
       }
       SUBPHASE_BEGIN
       coop_cast<false>(cv, qn, p, d, t, hit);
@@ -1118,8 +1159,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     if (active && hit < 0) {  // miss: the stale L_e/L_d are re-added (F4)
       finished = true;
       escaped = (k > 0);
-      if (MODE != MODE_GRAPH)
+      if (MODE != MODE_GRAPH) {
+        const V3 Le = le();
         L = mk(fmaf(M.x, Le.x + Ld.x, L.x), fmaf(M.y, Le.y + Ld.y, L.y), fmaf(M.z, Le.z + Ld.z, L.z));
+      }
     }
     const int tri = hit;
     V3 nh = p, din = d, sd = d, nd = d;
@@ -1136,7 +1179,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         const size_t bin = (size_t)dst * nT + tri;
         bins_add(a.lds_edges != 0, edges, a.lds_edges ? bin * kEdgeL : bin * kEdgeW, 5, v);
       } else if (k == 0) {
-        Le = ke3(tri);
+        set_le(ke3(tri));
       }
       nh = shading_normal(geom[tri], q);
       p = q;
@@ -1318,6 +1361,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           dst = tri;
         }
       } else {
+        const V3 Le = le();
         L = mk(fmaf(M.x, Le.x + Ld.x, L.x), fmaf(M.y, Le.y + Ld.y, L.y), fmaf(M.z, Le.z + Ld.z, L.z));
         if (cont) {
           const V3 tp = kdpi3(tri);
@@ -1332,7 +1376,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         }
       }
       ++k;  // vertices so far
-      if (BVH) ptri = tri;
+      if (BVH) set_ptri(tri);
       if (cont) d = nd;
       else finished = true;
       if (MODE == MODE_ADJU && rhi > 0 && k == rhi) finished = true;  // replay reached its target
@@ -1345,12 +1389,13 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     if (finished) {
       active = false;
       if (MODE == MODE_FWDM) {  // slot [channel][sample]
-        lds_f32 *o = fused_slots(a) + (uint32_t)(witem & 15u) * 3u * (uint32_t)a.spp + (uint32_t)(witem >> 4);
+        const uint64_t wi = witem();
+        lds_f32 *o = fused_slots(a) + (uint32_t)(wi & 15u) * 3u * (uint32_t)a.spp + (uint32_t)(wi >> 4);
         o[0] = L.x;
         o[a.spp] = L.y;
         o[2 * a.spp] = L.z;
       } else if (MODE == MODE_FWD) {
-        float *o = out_samples + witem * 3;
+        float *o = out_samples + witem() * 3;
         o[0] = L.x;
         o[1] = L.y;
         o[2] = L.z;
@@ -1382,13 +1427,13 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       __builtin_amdgcn_wave_barrier();
       uint32_t left = 0;
       if (finished)
-        left = __hip_atomic_fetch_sub(fused_tab(a) + (uint32_t)(witem & 15u), 1u, __ATOMIC_RELAXED,
+        left = __hip_atomic_fetch_sub(fused_tab(a) + (uint32_t)(witem() & 15u), 1u, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_WORKGROUP);
       uint64_t comp = __ballot(finished && left == 1u);
       while (comp) {  // wave-uniform: usually 0 or 1 slot per iteration
         const int l = (int)__builtin_ctzll(comp);
         comp &= comp - 1ull;
-        sdone |= 1u << (__builtin_amdgcn_readlane((int)(witem & 15u), l) & 31);
+        sdone |= 1u << (__builtin_amdgcn_readlane((int)(witem() & 15u), l) & 31);
       }
     }
     if (is_adj<MODE>()) {
@@ -1419,7 +1464,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         if (Kf > 0) {
           const float *adj = karg<const float *>(offsetof(TraceKernArgs, adj)) +
                              (a.nscenes > 1 ? (size_t)set * a.adj_stride : 0);
-          const uint64_t pixel = item_pixel(a, witem);
+          const uint64_t pixel = item_pixel(a, witem());
           if (a.rc_spp != 0.f) {
             wx = adj[pixel * 3 + 0] * a.rc_spp;
             wy = adj[pixel * 3 + 1] * a.rc_spp;
@@ -1460,7 +1505,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           const bool esc = valid && ((mk_ >> 13) & 1u);
           const bool fst_o = is_badj<MODE>() || (valid && ((mk_ >> 14) & 1u));  // the chunk ends the path
           const int rr = valid ? KL - 1 - kk : 0;  // vertices after this one
-          const V3 LeL = mk(__shfl(Le.x, ow), __shfl(Le.y, ow), __shfl(Le.z, ow));
+          const V3 Lev = le();
+          const V3 LeL = mk(__shfl(Lev.x, ow), __shfl(Lev.y, ow), __shfl(Lev.z, ow));
           // this task's record (lanes past the round read vertex 0 of a valid column)
           uint32_t f0;
           float es, ck, sdv = 0.f, si = 0.f;
@@ -1602,14 +1648,14 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       }
       if (MODE == MODE_ADJU && urep > 0) {  // replay the path from its camera ray (see the chunk choice)
         int r, c;
-        item_ray(a, seed, witem, st, p, d, r, c);
+        item_ray(a, seed, witem(), st, p, d, r, c);
         L = mk(0.f, 0.f, 0.f);
-        Le = L;
+        set_le(L);
         Ld = L;
         M = mk(1.f, 1.f, 1.f);
         Mlo = M;
         k = 0;
-        ptri = -1;
+        set_ptri(-1);
         rslot = 0;
         rhi = urep;
         active = true;
@@ -2087,7 +2133,8 @@ static bool use_bvh(const GpuScene *s) {
 // BVH LDS carve-out on top of `base` bytes; fills the args' BVH fields:
 // [wide nodes if staged][large pairs' plane offsets][large pairs' copy if
 // taken][emitter records][the wave's 8 group stacks].
-static size_t bvh_lds(const GpuScene *s, TraceArgs &a, size_t base, bool stage = true, bool big_copy = true) {
+static size_t bvh_lds(const GpuScene *s, TraceArgs &a, size_t base, bool stage = true, bool big_copy = true,
+                      bool lane_words = false) {
   const size_t nw = s->host.bvh_wide.size();
   a.bvh_wide = s->wide;
   a.bvh_wtris = s->wtris;
@@ -2102,7 +2149,8 @@ static size_t bvh_lds(const GpuScene *s, TraceArgs &a, size_t base, bool stage =
   const size_t head = bvh_lds_offset(base) + (size_t)a.bvh_wide_lds * kWideF4 * sizeof(float4) +
                       (size_t)a.bvh_nbig * 6 * sizeof(float) + (a.bvh_big_lds ? big_lds_bytes(a.bvh_nbig) : 0) +
                       emit_lds_bytes(s->host.nE);
-  return head + (size_t)(kBlock / 64) * 8 * a.coop_stride * sizeof(uint32_t);
+  return head + (size_t)(kBlock / 64) * 8 * a.coop_stride * sizeof(uint32_t) +
+         (lane_words ? (size_t)6 * kBlock * sizeof(uint32_t) : 0);  // (BVH forward: trace_kernel's lane_ws)
 }
 
 static size_t table_bytes(const TraceArgs &a) {
@@ -2345,7 +2393,7 @@ static int launch_bvh_pick(GpuScene *s, TraceArgs &a, size_t *lds, size_t tail) 
     int best = -1, best_per_cu = 0;
     for (int k = 0; k < 4; ++k) {
       TraceArgs b = a;
-      const size_t l = bvh_lds_offset(bvh_lds(s, b, base, opt[k][0], opt[k][1])) + tail;
+      const size_t l = bvh_lds_offset(bvh_lds(s, b, base, opt[k][0], opt[k][1], is_fwd<MODE>())) + tail;
       if (l > 160 * 1024) continue;
       int per_cu = 0;
       HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<MODE, SPEC, true>,
@@ -2364,7 +2412,7 @@ static int launch_bvh_pick(GpuScene *s, TraceArgs &a, size_t *lds, size_t tail) 
     s->pick_tail[slot] = tail;
   }
   const int k = s->pick_opt[slot];
-  *lds = bvh_lds(s, a, base, opt[k][0], opt[k][1]);
+  *lds = bvh_lds(s, a, base, opt[k][0], opt[k][1], is_fwd<MODE>());
   return 0;
 }
 

@@ -34,7 +34,7 @@ BUDGET = {
     (1, False, True): 0,    # BVH adjoint (2 waves/SIMD, 256 VGPRs allowed)
     (3, False, True): 0,
     (3, False, False): 16,  # unbounded adjoint: 3 spilled VGPRs
-    (0, False, True): 64,   # BVH forward at 5 waves/SIMD (spill outside the casts)
+    (0, False, True): 0,    # BVH forward: the work item, source triangle and Le in LDS (round 5; was 44-52 B)
     # SPEC instances (materials with a Phong lobe): pow_d out of line keeps its
     # constants out of the trace loop (round 4: 164-292 B per lane)
     (0, True, False): 16,
@@ -42,7 +42,7 @@ BUDGET = {
     (3, True, False): 32,
     (4, True, False): 32,
     (1, True, True): 0,
-    (0, True, True): 96,    # BVH forward + Phong at 5 waves/SIMD
+    (0, True, True): 32,    # BVH forward + Phong at 5 waves/SIMD
 }
 
 
