@@ -338,6 +338,67 @@ def test_mixed_launch_kinds_share_one_stream(scenes):
             hip.hipStreamDestroy(raw)
 
 
+def test_counter_reset_over_launch_shapes(scenes, oracle):
+    """The chunk counters reset themselves only if the host's count of a
+    launch's grabs (ipt_hip.hip launch_grabs) equals what the kernel's waves
+    do.  Launches of many shapes -- ragged frames, tiny and wide, fused
+    renders with 1..16-pixel groups, the unfused fallbacks (spp > 256, < 32
+    samples per group), row shares, bounded and unbounded adjoints, the BVH
+    instance's guided chunks -- run back to back on ONE stream into
+    NaN-filled buffers, each equal to the same launch on a fresh stream: a
+    counter left non-zero would make the next launch skip chunks."""
+    import torch
+
+    from conftest import NORTHSTAR
+    from inverse_path_tracer_amd import _native as N
+
+    L = N.lib()
+    hip = C.CDLL("libamdhip64.so")
+    ns = product_scene(NORTHSTAR)
+    objs = {"cornell": scenes["cornell"][0], "scene0": scenes["scene0"][0], "northstar": ns}
+    shapes = [("cornell", 1, 1, 1, 4), ("cornell", 7, 3, 5, 2), ("scene0", 33, 17, 64, 4), ("scene0", 100, 9, 100, None),
+              ("cornell", 13, 31, 256, 4), ("scene0", 5, 4, 300, 4), ("cornell", 16, 8, 2, 4), ("scene0", 64, 64, 16, 8),
+              ("northstar", 21, 19, 16, 4), ("northstar", 40, 8, 64, None), ("cornell", 129, 1, 3, 4),
+              ("scene0", 2, 77, 33, None), ("northstar", 3, 3, 1, 2)]
+    raws = []
+    try:
+        raw, st_shared = _stream(hip)
+        raws.append(raw)
+        runs = []
+        for name, W, H, spp, mb in shapes:
+            for rows in ((0, H, 1), (H // 3, H, 2)):
+                p = N.make_params(W, H, spp, mb, 11 + W, *rows)
+                np_ = ((rows[1] - rows[0] + rows[2] - 1) // rows[2]) * W
+                adj = torch.from_numpy(np.random.RandomState(W).uniform(-1, 1, (H, W, 3)).astype(np.float32)).cuda()
+                for kind in ("render", "adjoint"):
+                    def go(st, kind=kind, p=p, np_=np_, adj=adj, sc=objs[name]):
+                        if kind == "render":
+                            o = torch.full((max(np_, 1), 3), float("nan"), device="cuda")
+                            N.check(L.ipt_render_dev(sc.handle, C.byref(p), None, o.data_ptr(), None, st))
+                        else:
+                            o = torch.zeros((sc.nT, 3), device="cuda", dtype=torch.float64)
+                            N.check(L.ipt_adjoint_dev(sc.handle, C.byref(p), None, adj.data_ptr(), o.data_ptr(), st))
+                        return o
+                    runs.append(((name, W, H, spp, mb, rows, kind), go, np_))
+        got = [go(st_shared.cuda_stream) for _, go, _ in runs]
+        torch.cuda.synchronize()
+        for (key, go, np_), g in zip(runs, got):
+            raw, st = _stream(hip)
+            raws.append(raw)
+            w = go(st.cuda_stream)
+            torch.cuda.synchronize()
+            if key[-1] == "render":
+                assert not torch.isnan(g[:np_]).any(), key
+                assert torch.equal(g.view(torch.int32), w.view(torch.int32)), key
+            else:
+                np.testing.assert_allclose(g.cpu().numpy(), w.cpu().numpy(), rtol=1e-9, atol=1e-13, err_msg=str(key))
+    finally:
+        torch.cuda.synchronize()
+        ns.close()
+        for raw in raws:
+            hip.hipStreamDestroy(raw)
+
+
 def test_failed_launch_leaves_the_stream_usable(scenes):
     """A launch that fails after its chunk counters and scratch are allocated
     (ipt_debug_fail_launches: the error comes just before the kernel is
