@@ -11,9 +11,9 @@ vector only"): rank r traces rows r, r + N, ... of the SAME frame
 see `bands_*`; sample seeds are global indices, so the shares are the
 single-GPU frame's samples);
 the forward needs no collective, the adjoint step ends with ONE all-reduce of
-the nT*3 fp64 gradient.  Consecutive steps alternate between two HIP streams
-(two frames in flight, each with its own image / gradient buffer), so one
-frame's tail overlaps the next frame's start; `secondary.serial` is the same
+the nT*3 fp64 gradient.  Consecutive steps go round-robin over NSTREAMS = 3
+HIP streams (three frames in flight, each with its own image / gradient
+buffer), so one frame's tail overlaps the next frames' starts; `secondary.serial` is the same
 run on one stream.  Strong scaling: value = frame samples * K / (max
 over ranks of the time of K steps).  Inputs are resident in HBM before the
 timed region; timing is HIP events on the launch stream, bracketed by barrier
@@ -45,6 +45,12 @@ from inverse_path_tracer_amd.scene import ObjectSpec, Scene  # noqa: E402
 W = H = 512
 SPP = 64
 BOUNCES = 4
+# frames in flight of the headline: consecutive steps are dealt round-robin
+# over this many HIP streams (tools/streams_ab.py, profiles/r05/streams_ab_r05q.log:
+# C2 forward per frame 1.568 / 1.513 / 1.507 / 1.522 ms and adjoint 1.853 /
+# 1.780 / 1.758 / 1.782 ms on 1 / 2 / 3 / 4 streams -- the fourth shares a
+# hardware queue with torch's own)
+NSTREAMS = 3
 ASSETS = os.path.join(ROOT, "assets")
 CORNELL = [ObjectSpec(os.path.join(ASSETS, "CornellBox", "CornellBox-Empty-CO.obj"),
                       os.path.join(ASSETS, "CornellBox", "CornellBox-Empty-CO.mtl"), (0, 0, 4), (0, 0, 0), (2, 2, 2))]
@@ -251,17 +257,18 @@ class Leg:
         self.hdr = torch.empty((npix, 3), device=dev, dtype=torch.float32)
         self.adj = torch.full((h, w, 3), 1.0 / (3 * w * h), device=dev, dtype=torch.float32)
         self.grad = torch.zeros((self.sc.nT, 3), device=dev, dtype=torch.float64)
-        # frames in flight (piped=True): consecutive steps alternate between two
-        # streams, each with its own output image and gradient, so one frame's
-        # tail overlaps the next frame's start (the chunk counters are per stream)
+        # frames in flight (piped=True): consecutive steps go round-robin over
+        # NSTREAMS streams, each with its own output image and gradient, so one
+        # frame's tail overlaps the next frames' starts (the chunk counters are per stream)
         # (the headline's Leg is the process's first: HIP maps streams onto a
         # few hardware queues in creation order, and two streams sharing one
         # run in order; measured per-share overlap: tools/pipeline_ab.py)
-        # (streams: reuse another Leg's pair -- the per-share pipelined table
+        # (streams: reuse another Leg's streams -- the per-share pipelined table
         # runs on the headline's streams, the process's first)
-        self.streams = list(streams) if streams else [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
-        self.hdr2 = [self.hdr, torch.empty_like(self.hdr)]
-        self.grad2 = [self.grad, torch.zeros_like(self.grad)]
+        self.streams = list(streams) if streams else [torch.cuda.Stream(dev) for _ in range(NSTREAMS)]
+        ns = len(self.streams)
+        self.hdr2 = [self.hdr] + [torch.empty_like(self.hdr) for _ in range(ns - 1)]
+        self.grad2 = [self.grad] + [torch.zeros_like(self.grad) for _ in range(ns - 1)]
         self.kev = []
 
     def params(self, step):
@@ -273,7 +280,8 @@ class Leg:
         the per-pixel mean fused in (brute-force scenes; BVH scenes render
         through the sample buffer + pixel_mean_sm_kernel inside the same call)."""
         cx, p = self.cx, self.params(step)
-        st, hdr = (self.streams[step % 2], self.hdr2[step % 2]) if piped else (cx.stream, self.hdr)
+        k = step % len(self.streams)
+        st, hdr = (self.streams[k], self.hdr2[k]) if piped else (cx.stream, self.hdr)
         if ev is not None:
             ev[0].record(st)
         N.check(cx.L.ipt_render_dev(self.sc.handle, C.byref(p), None, hdr.data_ptr(), None, st.cuda_stream))
@@ -282,7 +290,8 @@ class Leg:
 
     def adjoint(self, step, reduce=True, piped=False):
         cx, p = self.cx, self.params(step)
-        st, grad = (self.streams[step % 2], self.grad2[step % 2]) if piped else (cx.stream, self.grad)
+        k = step % len(self.streams)
+        st, grad = (self.streams[k], self.grad2[k]) if piped else (cx.stream, self.grad)
         with torch.cuda.stream(st):
             grad.zero_()
             N.check(cx.L.ipt_adjoint_dev(self.sc.handle, C.byref(p), None, self.adj.data_ptr(), grad.data_ptr(),
@@ -317,8 +326,8 @@ def band_table(cx, objs, w, h, spp, mb, n=8, reps=2, interleaved=False):
 
 
 def band_table_piped(cx, objs, w, h, spp, mb, streams, n=8, reps=20):
-    """Each interleaved 1/n share of one frame with two frames in flight, the
-    headline's form (consecutive steps alternate between two streams), on the
+    """Each interleaved 1/n share of one frame with frames in flight, the
+    headline's form (consecutive steps round-robin over its streams), on the
     headline's own streams: HIP maps streams onto its few hardware queues in
     creation order, and two streams created late can share one and run in
     order.  Per share: ms per step over `reps` steps (forward, adjoint) and a
@@ -333,7 +342,7 @@ def band_table_piped(cx, objs, w, h, spp, mb, streams, n=8, reps=20):
             leg.adjoint(10**6 + i, reduce=False, piped=True)
         f = cx.timed(lambda i: leg.fwd(i, piped=True), reps, leg.streams) / reps
         a = cx.timed(lambda i: leg.adjoint(i, reduce=False, piped=True), reps, leg.streams) / reps
-        last = leg.hdr2[(reps - 1) % 2].clone()
+        last = leg.hdr2[(reps - 1) % len(leg.streams)].clone()
         ref = torch.empty_like(last)
         p = leg.params(reps - 1)
         N.check(cx.L.ipt_render_dev(leg.sc.handle, C.byref(p), None, ref.data_ptr(), None, cx.st))
@@ -346,7 +355,7 @@ def band_table_piped(cx, objs, w, h, spp, mb, streams, n=8, reps=20):
     return {"bands": rows, "reps": reps, "fwd_max_ms": max(fw), "adj_max_ms": max(ad),
             "fwd_max_over_mean": round(max(fw) / np.mean(fw), 4), "adj_max_over_mean": round(max(ad) / np.mean(ad), 4),
             "all_bitwise_equal": all(x["bitwise_equal"] for x in rows),
-            "workload": "interleaved 1/%d shares of the C2 frame, two frames in flight on the headline's two HIP "
+            "workload": "interleaved 1/%d shares of the C2 frame, frames in flight on the headline's HIP "
                         "streams; ms per step" % n}
 
 
@@ -421,15 +430,15 @@ def main():
     fwd_serial_ms = cx.timed(lambda i: head.fwd(i, kev[i]), args.steps)
     kernel_ms = float(np.mean([a.elapsed_time(z) for a, z in kev]))
     bwd_serial_ms = cx.timed(lambda i: head.adjoint(i), args.steps)
-    # (2) the headline: consecutive frames alternate between two streams (two
-    # frames in flight: one frame's tail -- its last paths, a few waves per
+    # (2) the headline: consecutive frames round-robin over NSTREAMS streams
+    # (frames in flight: one frame's tail -- its last paths, a few waves per
     # CU -- overlaps the next frame's start), the same K frames of work
     t_wall = time.perf_counter()
     fwd_ms = cx.timed(lambda i: head.fwd(i, piped=True), args.steps, head.streams)
     wall_fwd = time.perf_counter() - t_wall
-    # the last two frames in flight, re-rendered alone: bitwise the same images
-    last = list(range(max(0, args.steps - 2), args.steps))
-    got = {i: head.hdr2[i % 2].clone() for i in last}  # (hdr2[0] is head.hdr, which fwd(i) overwrites)
+    # the last NSTREAMS frames in flight, re-rendered alone: bitwise the same images
+    last = list(range(max(0, args.steps - len(head.streams)), args.steps))
+    got = {i: head.hdr2[i % len(head.streams)].clone() for i in last}  # (hdr2[0] is head.hdr, which fwd(i) overwrites)
     piped_ok = []
     for i in last:
         head.fwd(i)
@@ -454,7 +463,7 @@ def main():
                         "grad_ms_per_step": round(bwd_serial_ms / args.steps, 4),
                         "workload": "the headline's frames one after another on ONE stream (no frame overlap)"},
              "piped_frames_bitwise_equal_alone": piped_ok,
-             "headline_forward_form": ("two frames in flight" if all(piped_ok) else
+             "headline_forward_form": ("%d frames in flight" % len(head.streams) if all(piped_ok) else
                                        "INVALID in flight (frames differed from frames rendered alone): "
                                        "value is the one-stream rate")}
     if not args.no_secondary:
@@ -583,9 +592,9 @@ def main():
             "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": "C2: CornellBox-Empty-CO.obj, 512x512, 64 spp, max_bounces=4; one frame per step "
                                    "tiled over the ranks as interleaved rows (fwd); adjoint dL/dKd of the rank's rows "
-                                   "+ RCCL all-reduce of the gradient (grad); two frames in flight (consecutive steps "
-                                   "alternate between 2 HIP streams; one stream: secondary.serial)",
-                       "streams": 2 if piped_adj else "2 (fwd) / 1 (grad: gloo)",
+                                   "+ RCCL all-reduce of the gradient (grad); %d frames in flight (consecutive steps "
+                                   "round-robin over %d HIP streams; one stream: secondary.serial)" % (NSTREAMS, NSTREAMS),
+                       "streams": NSTREAMS if piped_adj else "%d (fwd) / 1 (grad: gloo)" % NSTREAMS,
                        "width": W, "height": H, "spp": SPP, "max_bounces": BOUNCES, "triangles": head.sc.nT,
                        "parallelism": "interleaved row tiles x%d" % world, "rank0_rows": [b, e, rs]},
             "grad_value": round(grad_value, 2), "grad_unit": "grad-Msamples/s",

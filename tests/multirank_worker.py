@@ -9,6 +9,8 @@ driver's one-rank-per-GPU RCCL run, same code path above the collective).
         unbounded adjoints through torch_ops.adjoint_into -> allreduce_; the
         differentiable torch_ops.render with row_step + backward -> allreduce_;
         createGraph through distributed.graph_sharded.  Rank 0 writes tile.pt.
+    python tests/multirank_worker.py rccl OUTDIR   (IPT_DIST_BACKEND=nccl, world 1)
+        the product's collectives through RCCL on its own device tensors.
     python tests/multirank_worker.py optimize OUTDIR
         C5's scene-parallel split (optimize.shard_scenes): a contiguous block of
         the scenes per rank, MaterialOptimizer(n_total=all scenes) for a few
@@ -117,15 +119,59 @@ def optimize(out):
                 for t in tasks}, os.path.join(out, "opt_%d.pt" % R))
 
 
+def rccl(out):
+    """One rank on RCCL (backend "nccl" on ROCm; a GPU takes one RCCL rank, so
+    the one-GPU box runs world 1): the collectives the product issues at N
+    ranks -- the fp64 gradient's all-reduce (torch_ops.adjoint_into's output),
+    the fp64 createGraph bins' all-reduce, an all-gather of an image band --
+    executed through RCCL on the product's own device tensors.  At world 1
+    they must return their inputs unchanged."""
+    import torch
+    import torch.distributed as dist
+
+    from conftest import SCENE0, product_scene
+    from inverse_path_tracer_amd import _native as N
+    from inverse_path_tracer_amd import torch_ops
+
+    c = CONFIG
+    assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
+    dev = torch.device("cuda", 0)
+    W, H, spp, mb, seed = c["W"], c["H"], c["spp"], c["mb"], c["seed"]
+    sc = product_scene(SCENE0)
+    adj, target = inputs(H, W, dev)
+    g = torch.zeros((sc.nT, 3), device=dev, dtype=torch.float64)
+    torch_ops.adjoint_into(sc, N.make_params(W, H, spp, mb, seed), None, adj.data_ptr(), g)
+    g0 = g.clone()
+    dist.all_reduce(g, op=dist.ReduceOp.SUM)
+    bins, _ = sc.graph(target, W, H, spp, None, seed)
+    b = torch.from_numpy(bins).to(dev)
+    b0 = b.clone()
+    dist.all_reduce(b, op=dist.ReduceOp.SUM)
+    hdr = torch.empty((H, W, 3), device=dev, dtype=torch.float32)
+    torch_ops.render_into(sc, N.make_params(W, H, spp, mb, seed), None, hdr)
+    outs = [torch.empty_like(hdr)]
+    dist.all_gather(outs, hdr)
+    torch.cuda.synchronize()
+    res = {"grad_equal": bool(torch.equal(g, g0)), "bins_equal": bool(torch.equal(b, b0)),
+           "gather_equal": bool(torch.equal(outs[0].view(torch.int32), hdr.view(torch.int32))),
+           "grad_nonzero": bool(g0.abs().max().item() > 0)}
+    torch.save(res, os.path.join(out, "rccl.pt"))
+    sc.close()
+
+
 def main():
     import torch
     import torch.distributed as dist
 
     mode, out = sys.argv[1], sys.argv[2]
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo")
+    backend = os.environ.get("IPT_DIST_BACKEND", "gloo")
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group(backend)
     try:
-        {"tile": tile, "optimize": optimize}[mode](out)
+        {"tile": tile, "optimize": optimize, "rccl": rccl}[mode](out)
         dist.barrier()
     finally:
         dist.destroy_process_group()

@@ -30,13 +30,13 @@ def _free_port():
     return port
 
 
-def _launch(mode, out, world=2, timeout=240):
+def _launch(mode, out, world=2, timeout=240, backend="gloo"):
     """Start `world` ranks as child processes (never a re-exec of this one) and wait for all."""
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port))
+                   MASTER_PORT=str(port), IPT_DIST_BACKEND=backend)
         procs.append(subprocess.Popen([sys.executable, "-u", WORKER, mode, str(out)], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     logs = []
@@ -131,3 +131,14 @@ def test_two_rank_scene_parallel_adam_equals_one_rank(tmp_path):
         np.testing.assert_allclose(g["history"], t.history, rtol=1e-5)
         np.testing.assert_allclose(g["kd"].numpy(), t.kd.detach().cpu().numpy(), rtol=0, atol=1e-6)
         assert not np.allclose(g["kd"].numpy(), 0.5)  # the parameters moved
+
+
+def test_rccl_collectives_on_product_tensors(tmp_path):
+    """RCCL itself (backend "nccl" on ROCm) on this one-GPU box: one rank
+    (a GPU takes one RCCL rank), the collectives the N-rank path issues --
+    all-reduce of the fp64 gradient and of the createGraph bins, all-gather of
+    an image band -- on the product's device tensors; at world 1 they return
+    their inputs.  (The driver's 8-GPU run is the multi-rank RCCL case.)"""
+    _launch("rccl", tmp_path, world=1, backend="nccl")
+    res = torch.load(str(tmp_path / "rccl.pt"), weights_only=True)
+    assert res == {"grad_equal": True, "bins_equal": True, "gather_equal": True, "grad_nonzero": True}, res
