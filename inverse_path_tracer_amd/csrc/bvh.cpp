@@ -619,8 +619,9 @@ static bool build_wide(HostScene *S) {
 //    within 2^-23 R of the exact ray point, and inside A_w, where n_s.(x -
 //    c_s) <= M_s = the largest value over all A_w's vertices.  So when
 //    1e-2 (n_s.d) > M_s + h + 2^-23 R, no tree triangle can accept the ray:
-//    tau_s = (M_s + h + 2^-23 R) / 1e-2 + 2e-6 (the fp32 dot's error), the
-//    kernel skips the tree when dot(n_s, d) >= tau_s.  Every tree triangle
+//    tau_s = (M_s + h + 2^-23 R) / 1e-2 + 2e-6 (the fp32 dot's error), and
+//    at least 4e-6 (the bound needs n_s.d >= 0); the kernel skips the tree
+//    when dot(n_s, d) >= tau_s.  Every tree triangle
 //    behind s's plane -- a convex mesh's own faces seen from any of them, or
 //    an object behind a wall -- gives tau_s < 1; otherwise tau_s = +inf.
 //    (North-star scene: every path and shadow ray leaving the sphere.)
@@ -657,7 +658,10 @@ static void tree_cull(HostScene *S, const std::vector<Prim> &tree, double r_all)
     for (int a = 0; a < 3; ++a) finite = finite && std::isfinite(n[a]) && std::isfinite(T.c[a]);
     for (size_t k = 0; k < nv && finite; ++k)
       m = std::max(m, n[0] * (vx[3 * k] - T.c[0]) + n[1] * (vx[3 * k + 1] - T.c[1]) + n[2] * (vx[3 * k + 2] - T.c[2]));
-    const double tau = (m + h + std::ldexp(r_all, -23) + 1e-9 * r_all) / 1e-2 + 2e-6;
+    // (the bound used t (n_s.d) >= 1e-2 (n_s.d), i.e. n_s.d >= 0: tau is at
+    // least 4e-6 even when the whole tree lies far behind s's plane -- a ray
+    // leaving s backwards may well reach it)
+    const double tau = std::max((m + h + std::ldexp(r_all, -23) + 1e-9 * r_all) / 1e-2 + 2e-6, 4e-6);
     for (int a = 0; a < 3; ++a) S->bvh_src_cull[(size_t)si * 4 + a] = T.n[a];
     S->bvh_src_cull[(size_t)si * 4 + 3] = (finite && nv > 0 && tau < 0.999) ? round_up(tau) : inf;
   }

@@ -942,9 +942,21 @@ def test_tree_entry_culls_equal_brute_force(which):
     aim += rng.normal(0, 0.03, (m, 3))
     Dr = aim - Or
     Dr /= np.linalg.norm(Dr, axis=1, keepdims=True)
-    O = np.concatenate([O, Or]).astype(np.float32)
-    D = np.concatenate([D, Dr]).astype(np.float32)
-    S = np.concatenate([src, np.full(m, -1)]).astype(np.int32)
+    # rays from points on every triangle towards points on the objects, in
+    # either hemisphere of the source: from faces with the whole tree behind
+    # them, the backward ones do reach it (the skip needs dot(n_s, d) > 0)
+    q = 60000
+    s2 = rng.randint(0, P.nT, q)
+    a3, b3 = rng.uniform(0, 1, (2, q))
+    flip = a3 + b3 > 1
+    a3[flip], b3[flip] = 1 - a3[flip], 1 - b3[flip]
+    O2 = v[s2, 0] + a3[:, None] * (v[s2, 1] - v[s2, 0]) + b3[:, None] * (v[s2, 2] - v[s2, 0])
+    k2 = rng.randint(18, P.nT, q)
+    D2 = v[k2].mean(1) - O2
+    D2 /= np.maximum(np.linalg.norm(D2, axis=1, keepdims=True), 1e-30)
+    O = np.concatenate([O, Or, O2]).astype(np.float32)
+    D = np.concatenate([D, Dr, D2]).astype(np.float32)
+    S = np.concatenate([src, np.full(m, -1), s2]).astype(np.int32)
     tg = np.full(len(O), -1, np.int32)
     tc, ic = P.shadow_hit(O, D, tg, S)  # the megakernel's BVH path cast with the source triangle
     P.set_accel(N.ACCEL_BRUTE)
