@@ -1,7 +1,7 @@
 """Per-kernel durations from a rocprofv3 --kernel-trace CSV, split into the
 launches that ran alone (no other launch of a trace kernel overlapping them:
 bench.py's serial pass, whose HIP-event time is `roofline.kernel_ms`) and
-those that overlapped another (the headline's two-frames-in-flight pass).
+those that overlapped another (the headline's frames-in-flight pass).
 
     python tools/prof_split.py gpurun_out/prof_X/run_kernel_trace.csv [out.json]
 """
