@@ -970,6 +970,79 @@ __device__ __forceinline__ float wave_shl1(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, true));
 }
 
+// One step of the adjoint sweep's two neighbour chains (ipt_hip.hip, the
+// wave-parallel sweep), with the wave shifts fused into the VALU operations
+// that consume them (the compiler keeps them as separate DPP moves and packs
+// the products into v_pk_mul_f32, which issues at half rate: 27 VALU slots
+// per step instead of these 18-20).  Same IEEE operations, same order:
+//  chain_step_shifted (operands pre-shifted once per round, loop-invariant
+//  keep masks; ADJ / ADJW):
+//    m = keepM ? m : (shr(m) * tl) * cl        s = keepS ? s : al + shl(s) * bl
+//  chain_step_select (ADJU: a lane takes its neighbour's product at its step):
+//    m = (km == i) ? shr((m * t) * c) : m      s = (kr == i) ? shl(a + b * s) : s
+// shr / shl read lane i-1 / i+1 (wave_shr:1 / wave_shl:1), 0 at the wave's
+// edge, as wave_shr1 / wave_shl1.  A DPP source written by a VALU needs two
+// wait states: the shifted form's sources are the previous step's selects
+// (the leading s_nop), the select form's are written >= 2 instructions before.
+__device__ __forceinline__ void chain_step_shifted(float &mx, float &my, float &mz, float &sx, float &sy, float &sz,
+                                                   V3 tl, float cl, V3 al, V3 bl, uint64_t keepM, uint64_t keepS) {
+  float t0, t1, t2, u0, u1, u2;
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_mul_f32_dpp %6, %0, %12 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_mul_f32_dpp %7, %1, %13 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_mul_f32_dpp %8, %2, %14 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_mul_f32_dpp %9, %3, %19 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_mul_f32_dpp %10, %4, %20 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_mul_f32_dpp %11, %5, %21 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_mul_f32_e32 %6, %6, %15\n\t"
+      "v_mul_f32_e32 %7, %7, %15\n\t"
+      "v_mul_f32_e32 %8, %8, %15\n\t"
+      "v_add_f32_e32 %9, %16, %9\n\t"
+      "v_add_f32_e32 %10, %17, %10\n\t"
+      "v_add_f32_e32 %11, %18, %11\n\t"
+      "v_cndmask_b32_e64 %0, %6, %0, %22\n\t"
+      "v_cndmask_b32_e64 %1, %7, %1, %22\n\t"
+      "v_cndmask_b32_e64 %2, %8, %2, %22\n\t"
+      "v_cndmask_b32_e64 %3, %9, %3, %23\n\t"
+      "v_cndmask_b32_e64 %4, %10, %4, %23\n\t"
+      "v_cndmask_b32_e64 %5, %11, %5, %23"
+      : "+v"(mx), "+v"(my), "+v"(mz), "+v"(sx), "+v"(sy), "+v"(sz), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(u0),
+        "=&v"(u1), "=&v"(u2)
+      : "v"(tl.x), "v"(tl.y), "v"(tl.z), "v"(cl), "v"(al.x), "v"(al.y), "v"(al.z), "v"(bl.x), "v"(bl.y), "v"(bl.z),
+        "s"(keepM), "s"(keepS));
+}
+__device__ __forceinline__ void chain_step_select(float &mx, float &my, float &mz, float &sx, float &sy, float &sz,
+                                                  V3 t, float c, V3 a, V3 b, int km, int kr, int i) {
+  float t0, t1, t2, u0, u1, u2;
+  asm volatile(
+      "v_mul_f32_e32 %6, %0, %12\n\t"
+      "v_mul_f32_e32 %7, %1, %13\n\t"
+      "v_mul_f32_e32 %8, %2, %14\n\t"
+      "v_mul_f32_e32 %9, %3, %19\n\t"
+      "v_mul_f32_e32 %10, %4, %20\n\t"
+      "v_mul_f32_e32 %11, %5, %21\n\t"
+      "v_mul_f32_e32 %6, %6, %15\n\t"
+      "v_mul_f32_e32 %7, %7, %15\n\t"
+      "v_mul_f32_e32 %8, %8, %15\n\t"
+      "v_add_f32_e32 %9, %16, %9\n\t"
+      "v_add_f32_e32 %10, %17, %10\n\t"
+      "v_add_f32_e32 %11, %18, %11\n\t"
+      "v_cmp_ne_u32_e32 vcc, %24, %22\n\t"
+      "v_cndmask_b32_dpp %0, %6, %0, vcc wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_cndmask_b32_dpp %1, %7, %1, vcc wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_cndmask_b32_dpp %2, %8, %2, vcc wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_cmp_ne_u32_e32 vcc, %24, %23\n\t"
+      "v_cndmask_b32_dpp %3, %9, %3, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_cndmask_b32_dpp %4, %10, %4, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_cndmask_b32_dpp %5, %11, %5, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+      : "+v"(mx), "+v"(my), "+v"(mz), "+v"(sx), "+v"(sy), "+v"(sz), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(u0),
+        "=&v"(u1), "=&v"(u2)
+      : "v"(t.x), "v"(t.y), "v"(t.z), "v"(c), "v"(a.x), "v"(a.y), "v"(a.z), "v"(b.x), "v"(b.y), "v"(b.z), "v"(km),
+        "v"(kr), "s"(i)
+      : "vcc");
+}
+
 // Minimum of a 32-bit int over the 8 lanes of each group: three DPP stages
 // (quad_perm [1,0,3,2]: lane ^ 1, [2,3,0,1]: lane ^ 2, row_half_mirror: the
 // other quad), each fused by the compiler into one v_min_i32_dpp.

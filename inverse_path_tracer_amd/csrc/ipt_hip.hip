@@ -135,6 +135,9 @@ constexpr int kMaxAdjBounces = 62;
 // §10.3).  Round 2 kept an 8-slot ring in LDS (24 KB
 // per workgroup): every path longer than 8 vertices replayed, C3 unbounded
 // adjoint 5.97 ms for a 2.73 ms forward.
+#ifndef IPT_CHAIN_DPP  // the sweep's chain steps with the wave shifts fused into their VALU ops (ipt_device.h)
+#define IPT_CHAIN_DPP 1
+#endif
 #ifndef IPT_ADJU_SHIFTED_CHAIN  // the bounded adjoint's chain form in MODE_ADJU too (A/B)
 #define IPT_ADJU_SHIFTED_CHAIN 0
 #endif
@@ -1588,6 +1591,12 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
               const V3 Al = mk(wave_shl1(A.x), wave_shl1(A.y), wave_shl1(A.z));
               const V3 Bl = mk(wave_shl1(B.x), wave_shl1(B.y), wave_shl1(B.z));
               const bool keepM = kkp == 0, keepS = rr == 0;
+#if IPT_CHAIN_DPP
+              const uint64_t kM = __ballot(keepM), kS = __ballot(keepS);
+              do {
+                chain_step_shifted(mx, my, mz, sx, sy, sz, tvl, ckl, Al, Bl, kM, kS);
+              } while (__ballot(steps > s++));
+#else
               do {  // (a do-while: the loop-carried values need no copies per step)
                 const float nx = (wave_shr1(mx) * tvl.x) * ckl, ny = (wave_shr1(my) * tvl.y) * ckl,
                             nz = (wave_shr1(mz) * tvl.z) * ckl;
@@ -1600,7 +1609,13 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
                 sy = keepS ? sy : hy;
                 sz = keepS ? sz : hz;
               } while (__ballot(steps > s++));
+#endif
             } else {  // ADJU (register pressure: no pre-shifted operands; a lane takes its neighbour's value at step kk / rr)
+#if IPT_CHAIN_DPP
+              do {
+                chain_step_select(mx, my, mz, sx, sy, sz, tv, ck, A, B, kkp, rr, s);
+              } while (__ballot(steps > s++));
+#else
               do {
                 const float nx = wave_shr1((mx * tv.x) * ck), ny = wave_shr1((my * tv.y) * ck),
                             nz = wave_shr1((mz * tv.z) * ck);
@@ -1614,6 +1629,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
                 sy = ts ? hy : sy;
                 sz = ts ? hz : sz;
               } while (__ballot(steps > s++));
+#endif
             }
             Mk = mk(mx, my, mz);
             S = mk(sx, sy, sz);
