@@ -117,9 +117,9 @@ constexpr int kMaxAdjBounces = 62;
 // (profiles/r04/unbounded_pmc_r04g.txt) -- and the unbounded adjoint took 1.7x
 // the unbounded forward.  Now the first IPT_ADJU_LDS_SLOTS slots of every lane
 // are in LDS (a path of up to 8 vertices never touches global memory) and the
-// rest of the ring is global: as many slots as IPT_ADJU_RING_MB (256 MB) holds
-// for the launch's resident lanes, up to IPT_ADJU_RING = 63 slots in all (63
-// at C3: 7 + 56, 327 680 lanes).  The ring's size is what bounds the
+// rest of the ring is global, IPT_ADJU_RING = 63 slots in all (round 4: 56
+// global slots per lane, 220 MB at C3 for 327 680 resident lanes; now pool
+// chunks per wave, below).  The ring's size is what bounds the
 // launch's tail: a path longer than the ring replays from its camera ray, and
 // the longest paths of a launch (~65 vertices in 16.8 M Russian-roulette
 // paths) then run alone at its end -- a 24-slot ring (64 MB) left the average
@@ -144,8 +144,22 @@ constexpr int kMaxAdjBounces = 62;
 #ifndef IPT_ADJU_RING
 #define IPT_ADJU_RING 63
 #endif
-#ifndef IPT_ADJU_RING_MB
-#define IPT_ADJU_RING_MB 256
+// The ring's global slots come from a pool per wave, in chunks of
+// kPoolSlots slots handed out as a lane's path reaches them (a lane holds at
+// most kPoolMaxChunks, their ids packed 6 bits each in `ctab`, 63 = none).
+// Most lanes never leave the LDS slots (a path of K vertices uses
+// ceil((K - rec_lds) / 16) chunks), so a pool of up to 63 chunks
+// (TraceArgs::pool_chunks, sized to IPT_ADJU_POOL_MB) serves 64 lanes: 12 KB
+// per wave, 62 MB at C3 (5120 resident waves) for the 220 MB of round 4's
+// per-lane ring.  A lane that finds the pool empty makes its current slot
+// count its ring size for the rest of the path (its chunks stay aligned to it,
+// the usual replays follow) -- with 4 LDS slots (the BVH instances) and 32
+// chunks that happened to 0.8% of the paths of a q = 0.8 simulation, and the
+// north star's unbounded adjoint lost 3%; with 48 or more, never
+// (tests/test_adju_protocol.py models the hand-out).
+constexpr int kPoolSlots = 16, kPoolMaxChunks = 4;
+#ifndef IPT_ADJU_POOL_MB
+#define IPT_ADJU_POOL_MB 64
 #endif
 // LDS ring slots only while the workgroup's LDS stays under this (bytes): at
 // equal occupancy (5 blocks/CU) scenes/0's unbounded adjoint ran 4.33 ms with
@@ -255,11 +269,12 @@ struct TraceArgs {
   float rc_W, rc_H;  // 1/W, 1/H for power-of-two sizes, else 0 (camera_ray divides)
   int rec_cap;   // ADJ: vertex records per lane (max_bounces + 1); ADJU: ring slots
   // ADJU: ring slots 0 .. rec_lds-1 of every lane live in LDS ([field][slot]
-  // [lane], like ADJ's records), slots rec_lds .. rec_cap-1 in global memory
-  // (grec: grec_stride lanes x (rec_cap - rec_lds) slots x fields)
+  // [lane], like ADJ's records), slots rec_lds .. rec_cap-1 in pool chunks in
+  // global memory (grec: grec_stride floats per wave, pool_chunks chunks)
   int rec_lds;
   float *grec;
   uint64_t grec_stride;
+  int pool_chunks;  // ADJU: chunks per wave pool (<= 63)
   // scene batch (C5): blocks b, b + nscenes, ... (bps of them) trace material
   // set b -- interleaved, not contiguous ranges: the dispatcher fills a CU
   // with consecutive workgroups, so contiguous ranges gave some sets fewer
@@ -821,18 +836,15 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     }
   };
 
-  // MODE_ADJU: the ring's global slots (TraceArgs::grec, [lane of the grid]
-  // [slot][field]: ustride floats per lane, a record's fields contiguous -- one
-  // 12-B store per vertex, and a sweep round reads an owner's consecutive
-  // records as one contiguous run.  Round 4's first form, [field][slot][lane],
+  // MODE_ADJU: the ring's global slots (TraceArgs::grec): this wave's pool of
+  // pool_chunks chunks, [chunk][slot][field], a record's fields contiguous --
+  // one 12-B store per vertex, and a sweep round reads an owner's consecutive
+  // records as contiguous runs.  Round 4's first form, [field][slot][lane],
   // stored 4 B per field at a different place per lane: three write requests
   // per vertex, 767 MB written per C3 launch, profiles/r04/unbounded_pmc_r04l.txt)
-  gbl_f32 *urec = nullptr;
-  size_t ustride = 0;
-  if (MODE == MODE_ADJU) {
-    ustride = (size_t)(a.rec_cap - a.rec_lds) * (SPEC ? kRecFieldsSpec : kRecFieldsDiffuse);
-    urec = (gbl_f32 *)a.grec + ((size_t)blockIdx.x * kBlock + tid) * ustride;
-  }
+  gbl_f32 *upool = nullptr;  // this wave's chunk pool ([chunk][slot][field])
+  if (MODE == MODE_ADJU)
+    upool = (gbl_f32 *)a.grec + ((size_t)blockIdx.x * (kBlock / 64) + (tid >> 6)) * a.grec_stride;
   {  // the wave's persistent loop
   // wave-uniform sample range (static partition, regenerated per lane)
   // XCD region (TraceArgs::nreg) of this block, and the wave's index among
@@ -904,6 +916,13 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   // starting at vertex 0; captured while a replay passes its start)
   V3 Scar = mk(0.f, 0.f, 0.f), Mlo = mk(1.f, 1.f, 1.f);
   int rhi = 0, rslot = 0;
+  // ADJU: the pool chunks this path holds and its ring size, in one word --
+  // bits 6j..6j+5: the id of its chunk j (63: none), 24-29: the ring size
+  // (a.rec_cap unless the pool ran dry) -- and the wave's free chunks
+  constexpr uint32_t kNoChunks = 0x00ffffffu;
+  uint32_t ctab = kNoChunks | ((uint32_t)vmax << 24);
+  uint64_t pfree = MODE == MODE_ADJU ? (a.pool_chunks >= 64 ? ~0ull : (1ull << a.pool_chunks) - 1ull) : 0ull;
+  auto vcap_of = [&]() { return (int)(ctab >> 24); };
   float weight = 1.f;  // GRAPH path weight
   V3 pix = p;          // GRAPH target pixel
   int k = 0, dst = 0;
@@ -1117,6 +1136,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             rhi = 0;
             rslot = 0;
             Mlo = mk(1.f, 1.f, 1.f);
+            ctab = kNoChunks | ((uint32_t)vmax << 24);
           }
           if (MODE == MODE_GRAPH) {
             weight = 1.f;
@@ -1318,6 +1338,34 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     }
 
     PHASE(4)
+    if (MODE == MODE_ADJU) {
+      // a lane about to write the first slot of a pool chunk it does not hold
+      // takes one (wave-uniform hand-out in lane order); none left: the ring
+      // ends here for this path (rslot = k, no wrap yet, so the path's chunks
+      // [j vcap, (j+1) vcap) stay aligned) and this record goes to slot 0
+      const int gs = rslot - a.rec_lds;
+      const int sh = 6 * (gs / kPoolSlots);
+      const bool needc = vertex && gs >= 0 && (gs % kPoolSlots) == 0 && ((ctab >> sh) & 63u) == 63u;
+      uint64_t want = __ballot(needc);
+      if (want) {
+        int got = -1;
+        do {
+          const int l = (int)__builtin_ctzll(want);
+          want &= want - 1;
+          const int c = pfree ? (int)__builtin_ctzll(pfree) : -1;
+          pfree &= pfree - 1ull;
+          if (lane == l) got = c;
+        } while (want);
+        if (needc) {
+          if (got >= 0) {
+            ctab = (ctab & ~(63u << sh)) | ((uint32_t)got << sh);
+          } else {
+            ctab = (ctab & 0x00ffffffu) | ((uint32_t)rslot << 24);
+            rslot = 0;
+          }
+        }
+      }
+    }
     // ================= finalise the vertex
     if (vertex) {
       if (is_badj<MODE>()) {  // vertex record k (layout [field][vertex][lane])
@@ -1347,15 +1395,17 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           const size_t fs = (size_t)nl * kBlock;
 #pragma unroll
           for (int f = 0; f < NF; ++f) rec[f * fs] = v[f];
-        } else {  // global slot
-          gbl_f32 *rec = urec + (size_t)(rslot - nl) * NF;
+        } else {  // global slot: pool chunk (rslot - nl) / kPoolSlots of this lane
+          const int gs = rslot - nl;
+          const uint32_t c = (ctab >> (6 * (gs / kPoolSlots))) & 63u;
+          gbl_f32 *rec = upool + ((size_t)c * kPoolSlots + (size_t)(gs % kPoolSlots)) * NF;
 #pragma unroll
           for (int f = 0; f < NF; ++f) rec[f] = v[f];
         }
-        // a chunk starts at ring slot 0 (vertex j * rec_cap): the forward's M
+        // a chunk starts at ring slot 0 (vertex j * ring size): the forward's M
         // before the update of its first vertex is the chunk's Mlo
         if (rslot == 0) Mlo = M;
-        rslot = (rslot + 1 == vmax) ? 0 : rslot + 1;
+        rslot = (rslot + 1 == vcap_of()) ? 0 : rslot + 1;
       }
       if (MODE == MODE_GRAPH) {
         if (cont) {
@@ -1411,12 +1461,12 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         // the suffix carried from the chunk after (Scar), and so on to vertex 0.
         if (rhi == 0) {
           uhi = k;
-          ulo = k > 0 ? k - (rslot == 0 ? vmax : rslot) : 0;  // (rslot = K % rec_cap)
+          ulo = k > 0 ? k - (rslot == 0 ? vcap_of() : rslot) : 0;  // (rslot = K % ring size)
           uend = true;
           uesc = escaped;
         } else {
           uhi = rhi;
-          ulo = rhi - vmax;
+          ulo = rhi - vcap_of();
         }
         if (ulo > 0) urep = ulo;
       }
@@ -1530,15 +1580,17 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             const int sl = kk, nl = a.rec_lds;  // the vertex's ring slot (chunks start at slot 0)
             constexpr int NF = SPEC ? kRecFieldsSpec : kRecFieldsDiffuse;
             float rv[NF];
+            uint32_t cto = 0;  // the owner's pool chunks (uniform branch: its ds_bpermute sees every lane)
+            if (__ballot(sl >= nl)) cto = (uint32_t)__shfl((int)ctab, ow);
             if (sl < nl) {  // LDS slot (typed: ds_read, see bins_add)
               const lds_f32 *r = (const lds_f32 *)lds_rec + (tid & ~63) + (valid ? ow : lane) + (size_t)sl * kBlock;
               const size_t fl = (size_t)nl * kBlock;
 #pragma unroll
               for (int f = 0; f < NF; ++f) rv[f] = r[f * fl];
             } else {  // global slot
-              const gbl_f32 *r = (const gbl_f32 *)a.grec +
-                                 ((size_t)blockIdx.x * kBlock + (tid & ~63) + (valid ? ow : lane)) * ustride +
-                                 (size_t)(sl - nl) * NF;
+              const int gs = sl - nl;
+              const uint32_t c = (cto >> (6 * (gs / kPoolSlots))) & 63u;
+              const gbl_f32 *r = upool + ((size_t)c * kPoolSlots + (size_t)(gs % kPoolSlots)) * NF;
 #pragma unroll
               for (int f = 0; f < NF; ++f) rv[f] = r[f];
             }
@@ -1660,6 +1712,25 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             if (owns) Scar = Hs;
           }
           base = next;
+        }
+      }
+      if (MODE == MODE_ADJU) {  // a path swept to its first vertex gives its pool chunks back
+        const bool rel = finished && urep == 0 && (ctab & kNoChunks) != kNoChunks;
+        uint64_t rm = __ballot(rel);
+        if (rm) {
+          uint64_t mine = 0;
+#pragma unroll
+          for (int j = 0; j < kPoolMaxChunks; ++j) {
+            const uint32_t c = (ctab >> (6 * j)) & 63u;
+            if (c != 63u) mine |= 1ull << c;
+          }
+          do {
+            const int l = (int)__builtin_ctzll(rm);
+            rm &= rm - 1;
+            pfree |= (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mine, l) |
+                     ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mine >> 32), l) << 32);
+          } while (rm);
+          if (rel) ctab |= kNoChunks;
         }
       }
       if (MODE == MODE_ADJU && urep > 0) {  // replay the path from its camera ray (see the chunk choice)
@@ -2106,6 +2177,7 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.rec_lds = 0;
   a.grec = nullptr;
   a.grec_stride = 0;
+  a.pool_chunks = 0;
   a.chunk = 0;
   a.group = 0;
   a.chunk_small = 0;
@@ -2361,14 +2433,13 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
     if (stream_counters(s, st, words, &b.chunk_ctr, &cap_ctr.p)) return -1;
   }
   StreamScratch grec;  // ADJU: the vertex-record ring (TraceArgs::grec), freed behind the launch
-  if (MODE == MODE_ADJU) {  // the ring's global slots
-    b.grec_stride = (uint64_t)grid * kBlock;
+  if (MODE == MODE_ADJU) {  // the ring's global slots: one chunk pool per wave
     const size_t fields = SPEC ? kRecFieldsSpec : kRecFieldsDiffuse;
-    // the ring: the LDS slots, then as many global ones as the budget holds
-    const size_t per_slot = fields * (size_t)b.grec_stride * sizeof(float);
-    const size_t fit = ((size_t)IPT_ADJU_RING_MB << 20) / per_slot;
-    b.rec_cap = a.rec_lds + (int)std::max<size_t>(1, std::min<size_t>(fit, (size_t)(kAdjuRing - a.rec_lds)));
-    if (grec.alloc(fields * (size_t)(b.rec_cap - b.rec_lds) * b.grec_stride * sizeof(float), st)) return -1;
+    const size_t waves = (size_t)grid * (kBlock / 64), chunk = (size_t)kPoolSlots * fields * sizeof(float);
+    b.pool_chunks = (int)std::max<size_t>(16, std::min<size_t>(63, ((size_t)IPT_ADJU_POOL_MB << 20) / (waves * chunk)));
+    b.grec_stride = (uint64_t)b.pool_chunks * kPoolSlots * fields;  // floats per wave
+    b.rec_cap = std::min(kAdjuRing, a.rec_lds + kPoolMaxChunks * kPoolSlots);
+    if (grec.alloc(waves * b.grec_stride * sizeof(float), st)) return -1;
     b.grec = (float *)grec.p;
   }
   // (tests: a launch that fails after its counters and scratch are allocated)
@@ -2656,7 +2727,9 @@ int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const f
       }
       nl = s->adju_nl;
     }
-    a.rec_lds = std::max(0, std::min(nl, kAdjuRing - 1));  // (launch_inst sizes the global part)
+    // (>= 1: a lane's first record never waits for a pool chunk; launch_inst
+    // sizes the global part)
+    a.rec_lds = std::max(1, std::min(nl, kAdjuRing - 1));
   }
   const size_t lds = base + (size_t)(unbounded ? a.rec_lds : a.rec_cap) * fields * kBlock * sizeof(float);
   if (lds > 160 * 1024) {

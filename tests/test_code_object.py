@@ -33,7 +33,7 @@ BUDGET = {
     (2, False, True): 0,
     (1, False, True): 0,    # BVH adjoint (2 waves/SIMD, 256 VGPRs allowed)
     (3, False, True): 0,
-    (3, False, False): 16,  # unbounded adjoint: 3 spilled VGPRs
+    (3, False, False): 8,   # unbounded adjoint: 1 spilled VGPR (pool chunks, round 5; was 3)
     (0, False, True): 0,    # BVH forward: the work item, source triangle and Le in LDS (round 5; was 44-52 B)
     # SPEC instances (materials with a Phong lobe): pow_d out of line keeps its
     # constants out of the trace loop (round 4: 164-292 B per lane)
