@@ -66,8 +66,8 @@ void setMaterials(void *scenePtr, float *materials);
  * row_step 1 = a contiguous band, row_step = world = a rank's interleaved
  * share); images and sample buffers hold those rows, in that order.
  * ABI 2 added row_step; ABI 3 dropped the quantised-node export of
- * ipt_scene_export_wide; ABI 4 added ipt_debug_fail_launches
- * (ipt_abi_version).  Bindings must check the version
+ * ipt_scene_export_wide; ABI 4 added ipt_debug_fail_launches; ABI 5 added
+ * ipt_debug_adju_ring (ipt_abi_version).  Bindings must check the version
  * before passing this struct. */
 typedef struct ipt_params {
   int32_t width, height, spp, max_bounces;
@@ -78,7 +78,7 @@ typedef struct ipt_params {
 
 const char *ipt_last_error(void);
 void ipt_clear_error(void);
-int ipt_abi_version(void);            /* 4 */
+int ipt_abi_version(void);            /* 5 */
 int ipt_device_count(void);
 /* Diagnostic: bitwise self-test of the kernels' in-range sqrt/division cores
  * against the IEEE operations over n random operands per test; counts[8]
@@ -91,6 +91,13 @@ int ipt_selftest_math(uint64_t n, uint64_t seed, uint64_t *counts);
  * unaffected (the counters reset themselves on the device).  No reference
  * counterpart. */
 void ipt_debug_fail_launches(int n);
+/* Diagnostic (tests): the unbounded adjoint's record ring at reduced sizes --
+ * pool_chunks 16-slot chunks per wave pool (1..63) and lds_slots LDS slots
+ * per lane (>= 1); 0 restores the launch's own choice.  Small pools make
+ * lanes find the pool empty and shorten their rings (replays), the paths the
+ * default sizes almost never take.  Gradients are unchanged.  No reference
+ * counterpart. */
+void ipt_debug_adju_ring(int pool_chunks, int lds_slots);
 
 /* Legacy-symbol configuration (defaults 500, 500, 100, -1, seed -1 = time). */
 void ipt_legacy_config(int width, int height, int spp, int max_bounces, int64_t seed);

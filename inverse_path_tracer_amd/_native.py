@@ -18,7 +18,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ipt.h")
 TRI_EXPORT_STRIDE = 57
 ACC_WIDTH = 8
 # include/ipt.h ipt_abi_version(): the Params layout and signatures below are this version's
-ABI_VERSION = 4
+ABI_VERSION = 5
 # acceleration modes (include/ipt.h IPT_ACCEL_*)
 ACCEL_AUTO, ACCEL_BRUTE, ACCEL_BVH = 0, 1, 2
 
@@ -79,6 +79,7 @@ SIGNATURES = {
     "ipt_device_count": (C.c_int, []),
     "ipt_selftest_math": (C.c_int, [C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64)]),
     "ipt_debug_fail_launches": (None, [C.c_int]),
+    "ipt_debug_adju_ring": (None, [C.c_int, C.c_int]),
     "ipt_legacy_config": (None, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int64]),
     "ipt_load_scene": (C.c_int, [C.c_int, fp, fp, fp, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.POINTER(vp)]),
     "ipt_load_scene_host": (C.c_int, [C.c_int, fp, fp, fp, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p),

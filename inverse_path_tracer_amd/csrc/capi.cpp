@@ -91,13 +91,14 @@ extern "C" {
 
 const char *ipt_last_error(void) { return g_err.c_str(); }
 void ipt_clear_error(void) { g_err.clear(); }
-int ipt_abi_version(void) { return 4; }
+int ipt_abi_version(void) { return 5; }
 int ipt_device_count(void) { return ipt::gpu_device_count(); }
 int ipt_selftest_math(uint64_t n, uint64_t seed, uint64_t *counts) {
   if (!counts) return -1;
   return gpu_status(ipt::gpu_selftest_math(n, seed, counts));
 }
 void ipt_debug_fail_launches(int n) { ipt::gpu_debug_fail_launches(n); }
+void ipt_debug_adju_ring(int pool_chunks, int lds_slots) { ipt::gpu_debug_adju_ring(pool_chunks, lds_slots); }
 
 void ipt_legacy_config(int width, int height, int spp, int max_bounces, int64_t seed) {
   g_legacy.width = width;

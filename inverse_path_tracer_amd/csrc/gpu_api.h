@@ -59,6 +59,7 @@ int gpu_closest_hit_host(GpuScene *s, int64_t n, const float *org, const float *
 int gpu_device_count();
 int gpu_selftest_math(uint64_t n, uint64_t seed, uint64_t *counts);  // 8 mismatch counters
 void gpu_debug_fail_launches(int n);  // the next n trace launches fail before their kernel is enqueued
+void gpu_debug_adju_ring(int pool_chunks, int lds_slots);  // unbounded adjoint ring sizes (0: default)
 const char *gpu_last_error();
 void gpu_set_error(const std::string &e);
 

@@ -53,6 +53,14 @@ const char *gpu_last_error() { return g_gpu_err.c_str(); }
 // nothing behind that a later launch on the stream depends on
 static std::atomic<int> g_fail_launches{0};
 void gpu_debug_fail_launches(int n) { g_fail_launches.store(n > 0 ? n : 0); }
+// ipt_debug_adju_ring(chunks, slots): the unbounded adjoint's pool chunks per
+// wave and LDS slots per lane forced small (0: the launch's choice) -- the
+// tests' way to run the empty-pool and short-ring paths
+static std::atomic<int> g_adju_pool{0}, g_adju_lds{0};
+void gpu_debug_adju_ring(int pool_chunks, int lds_slots) {
+  g_adju_pool.store(pool_chunks > 0 ? std::min(pool_chunks, 63) : 0);
+  g_adju_lds.store(lds_slots > 0 ? lds_slots : 0);
+}
 
 #define HIP_TRY(expr)                                                                        \
   do {                                                                                       \
@@ -2437,6 +2445,7 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
     const size_t fields = SPEC ? kRecFieldsSpec : kRecFieldsDiffuse;
     const size_t waves = (size_t)grid * (kBlock / 64), chunk = (size_t)kPoolSlots * fields * sizeof(float);
     b.pool_chunks = (int)std::max<size_t>(16, std::min<size_t>(63, ((size_t)IPT_ADJU_POOL_MB << 20) / (waves * chunk)));
+    if (g_adju_pool.load() > 0) b.pool_chunks = g_adju_pool.load();
     b.grec_stride = (uint64_t)b.pool_chunks * kPoolSlots * fields;  // floats per wave
     b.rec_cap = std::min(kAdjuRing, a.rec_lds + kPoolMaxChunks * kPoolSlots);
     if (grec.alloc(waves * b.grec_stride * sizeof(float), st)) return -1;
@@ -2729,6 +2738,7 @@ int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const f
     }
     // (>= 1: a lane's first record never waits for a pool chunk; launch_inst
     // sizes the global part)
+    if (g_adju_lds.load() > 0) nl = g_adju_lds.load();
     a.rec_lds = std::max(1, std::min(nl, kAdjuRing - 1));
   }
   const size_t lds = base + (size_t)(unbounded ? a.rec_lds : a.rec_cap) * fields * kBlock * sizeof(float);

@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared_functions():
         assert hasattr(L, name), name
         assert name in N.SIGNATURES, "python binding lacks %s" % name
-    assert L.ipt_abi_version() == 4
+    assert L.ipt_abi_version() == 5
 
 
 @pytest.mark.parametrize("soname", ["libpt.so", "libipt.so"])

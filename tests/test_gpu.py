@@ -434,6 +434,38 @@ def test_failed_launch_leaves_the_stream_usable(scenes):
             np.testing.assert_allclose(g, want, rtol=1e-9, atol=1e-12)
 
 
+_TINY_POOL_WANT = {}
+
+
+@pytest.mark.parametrize("pool,lds", [(1, 1), (2, 1), (3, 2), (1, 4)])
+def test_unbounded_adjoint_with_tiny_record_pools(scenes, oracle, pool, lds):
+    """The unbounded adjoint's ring forced small with
+    ipt_debug_adju_ring: `pool` 16-slot chunks per wave and `lds` LDS slots
+    per lane.  Lanes then find the pool empty and make their current slot
+    count their ring size (1 or 17 slots...), so long paths replay from their
+    camera rays chunk by chunk -- paths the default sizes almost never take.
+    The gradient equals the oracle's (rtol 1e-9), on scenes/0 and the
+    north-star (BVH instance)."""
+    from inverse_path_tracer_amd import _native as N
+
+    from conftest import NORTHSTAR
+
+    L = N.lib()
+    adj = np.random.RandomState(4).uniform(-1, 1, (40, 48, 3)).astype(np.float32)
+    if "northstar" not in scenes:
+        scenes["northstar"] = (product_scene(NORTHSTAR), oracle.OracleScene(NORTHSTAR))
+    for name in ("scene0", "northstar"):
+        P, Q = scenes[name]
+        L.ipt_debug_adju_ring(pool, lds)
+        try:
+            g = P.adjoint(adj, 48, 40, 8, None, 77)
+        finally:
+            L.ipt_debug_adju_ring(0, 0)
+        if name not in _TINY_POOL_WANT:
+            _TINY_POOL_WANT[name] = Q.adjoint(48, 40, 8, None, 77, adj)
+        np.testing.assert_allclose(g, _TINY_POOL_WANT[name], rtol=1e-9, atol=1e-12, err_msg=name)
+
+
 def test_adjoint_row_bands_sum_to_full(scenes):
     from inverse_path_tracer_amd.distributed import shard_rows
 
