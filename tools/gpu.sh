@@ -29,7 +29,6 @@
 #   workflow     tools/workflow_at_size.py (pipeline all --n 100 + optimize --n 100)
 #   graphprof    rocprofv3 --kernel-trace --stats of createGraph at the reference config (tools/graph_prof.py)
 #   pipeab       tools/pipeline_ab.py (consecutive frames on one stream vs two)
-#   envab        tools/env_ab.py $ENVAB (launch-time switches from the environment, A/B)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 R=$(pwd)
@@ -99,7 +98,6 @@ run() {
     graphprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/graphprof_$T" -o run --output-format csv \
                    -- python3 "$R/tools/graph_prof.py" --steps 20 > "$OUT/graphprof_$T.log" 2>&1 ;;
     pipeab) timeout -k 10 300 python tools/pipeline_ab.py > "$OUT/pipeab_$T.log" 2>&1 ;;
-    envab) timeout -k 10 400 python tools/env_ab.py ${ENVAB:-base:} > "$OUT/envab_$T.log" 2>&1 ;;
     *) echo "unknown stage $1" >&2; return 2 ;;
   esac
 }
