@@ -500,6 +500,13 @@ __device__ __forceinline__ void item_ray(const TraceArgs &a, uint64_t seed, uint
 #ifndef IPT_MIN_BLOCKS_BVH_ADJ
 #define IPT_MIN_BLOCKS_BVH_ADJ 2
 #endif
+// The unbounded adjoint's BVH instance: its LDS (4 ring slots, the gradient
+// hot set, the tree stage) leaves room for 4 workgroups per CU, and at 131
+// VGPRs it ran 3 waves/SIMD; held to 128 (4 waves) it spills nothing and the
+// north-star unbounded adjoint runs 7.08 -> 6.4x ms.
+#ifndef IPT_MIN_BLOCKS_BVH_ADJU
+#define IPT_MIN_BLOCKS_BVH_ADJU 4
+#endif
 // The forward's BVH instance at 5 waves/SIMD (96 VGPRs, ~116 B of spill,
 // mostly outside the casts) beats 4 (121 VGPRs, none): sphere scene 9.92 ->
 // 9.48 ms (profiles/r01_variants_bvh_occupancy.log); 6 spills in the
@@ -509,7 +516,9 @@ __device__ __forceinline__ void item_ray(const TraceArgs &a, uint64_t seed, uint
 #endif
 template <int MODE, bool BVH>
 constexpr int min_blocks() {
-  return BVH ? (is_adj<MODE>() ? IPT_MIN_BLOCKS_BVH_ADJ : (is_fwd<MODE>() ? IPT_MIN_BLOCKS_BVH_FWD : IPT_MIN_BLOCKS_BVH))
+  return BVH ? (MODE == MODE_ADJU ? IPT_MIN_BLOCKS_BVH_ADJU
+                                  : (is_adj<MODE>() ? IPT_MIN_BLOCKS_BVH_ADJ
+                                                    : (is_fwd<MODE>() ? IPT_MIN_BLOCKS_BVH_FWD : IPT_MIN_BLOCKS_BVH)))
              : (is_fwd<MODE>() ? IPT_MIN_BLOCKS_FWD
                                 : (MODE == MODE_ADJU   ? IPT_MIN_BLOCKS_ADJU
                                    : MODE == MODE_ADJW ? IPT_MIN_BLOCKS_ADJW
