@@ -494,6 +494,9 @@ def main():
                  "(no per-sample buffer)"),
                 ("c3_northstar", NORTHSTAR, W, H, SPP, BOUNCES, "C3 as the north_star names it: Cornell + cube + "
                  "sphere.obj (assets/northstar.txt, 1310 triangles, BVH), 512x512, 64 spp, 4 bounces"),
+                ("c3_northstar_unbounded", NORTHSTAR, W, H, SPP, None, "the north-star scene (1310 triangles, BVH) with "
+                 "the reference's own estimator (no bounce cap), 512x512, 64 spp; two-kernel render; adjoint = record "
+                 "ring in LDS + per-wave chunk pools + chunk replay"),
                 ("bvh_sphere", SPHERE, W, H, SPP, BOUNCES, "Cornell + sphere.obj (1298 triangles, BVH), 512x512, 64 spp, 4 bounces"),
                 ("c4", SCENE0, 1024, 1024, 256, 8, "C4: scenes/0.txt, 1024x1024, 256 spp, 8 bounces")):
             if key != "c4":
