@@ -179,8 +179,11 @@ constexpr int kPoolSlots = 16, kPoolMaxChunks = 4;
 #ifndef IPT_ADJU_LDS_SLOTS
 #define IPT_ADJU_LDS_SLOTS 8
 #endif
+// (BVH instance, at 4 waves/SIMD since round 5: 6 slots -- north-star 6.43
+// -> 6.37 ms against 4; 7 loses the fourth workgroup, 7.13 ms;
+// profiles/r05/variants_bvh_adju_lds_slots*.log)
 #ifndef IPT_ADJU_LDS_SLOTS_BVH
-#define IPT_ADJU_LDS_SLOTS_BVH 4
+#define IPT_ADJU_LDS_SLOTS_BVH 6
 #endif
 #ifndef IPT_ADJU_LDS_SLOTS_FIXED
 #define IPT_ADJU_LDS_SLOTS_FIXED -1
