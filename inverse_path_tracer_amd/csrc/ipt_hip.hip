@@ -1621,8 +1621,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
               sdv = rv[kRecSD];
               si = rv[kRecSD + 1];
             }
-            Mk = mk(__shfl(Mlo.x, ow), __shfl(Mlo.y, ow), __shfl(Mlo.z, ow));
-            Sc = mk(__shfl(Scar.x, ow), __shfl(Scar.y, ow), __shfl(Scar.z, ow));
+            // (wave-uniform skips: a chunk from vertex 0 has Mlo = 1, and only
+            // replay chunks, which paths longer than the ring make, read Scar)
+            if (__ballot(owns && ulo > 0)) Mk = mk(__shfl(Mlo.x, ow), __shfl(Mlo.y, ow), __shfl(Mlo.z, ow));
+            if (__ballot(owns && !uend)) Sc = mk(__shfl(Scar.x, ow), __shfl(Scar.y, ow), __shfl(Scar.z, ow));
           }
           // (the min()s keep a mis-indexed record from reaching global memory out of bounds)
           const int tk = min((int)(f0 & 0xffffu), nT - 1);
@@ -1725,7 +1727,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             double *grad = karg<double *>(offsetof(TraceKernArgs, grad)) + (a.nscenes > 1 ? (size_t)set * 3 * a.nT : 0);
             bins_add(sl >= 0, grad, sl >= 0 ? (size_t)sl * 3 : (size_t)tk * 3, 3, v);
           }
-          if (MODE == MODE_ADJU) {  // the suffix at the chunk's first vertex, S_lo = A + B S, back to its owner
+          if (MODE == MODE_ADJU && __ballot(owns && urep > 0)) {  // the suffix at the chunk's first vertex, S_lo = A + B S, back to its owner (for its replay)
             const V3 H = mk(A.x + B.x * S.x, A.y + B.y * S.y, A.z + B.z * S.z);
             const int sa = (owns ? st0 : lane) << 2;
             const V3 Hs = mk(bperm_f(sa, H.x), bperm_f(sa, H.y), bperm_f(sa, H.z));
