@@ -16,6 +16,7 @@
 #   attr         memory-side request classes of the C2 headline (atomics vs reads vs writes, TCC/TCP)
 #   valumix      VALU instruction-mix counter passes of the C2 headline
 #   uprof        kernel stats + FETCH/WRITE/TCC passes of the unbounded legs (tools/unbounded_prof.py)
+#   usq          SQ counter passes of the unbounded legs
 #   nsprof       rocprofv3 --kernel-trace --stats of the north-star scene (BVH instances)
 #   nspmc        FETCH/WRITE + SQ counter passes of the north-star scene
 #   scenes       tools/bench_scenes.py ($SCENES, default all)
@@ -79,6 +80,7 @@ run() {
                -- "${UP[@]}" > "$OUT/uprof_$T.log" 2>&1 &&
            SETS=$'FETCH_SIZE\nWRITE_SIZE\nTCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum' pmc_passes upmc "${UP[@]}" --steps 2 ;;
     valumix) SETS=$MIX_SETS pmc_passes valumix "${BENCHQ[@]}" ;;
+    usq) SETS=$SQ_SETS pmc_passes usq "${UP[@]}" --steps 2 ;;
     nsprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/nsprof_$T" -o run --output-format csv \
                 -- "${NS[@]}" --steps 10 > "$OUT/nsprof_$T.log" 2>&1 ;;
     nspmc) SETS=$'FETCH_SIZE\nWRITE_SIZE\n'"$SQ_SETS" pmc_passes nspmc "${NS[@]}" --steps 2 ;;
