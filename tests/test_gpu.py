@@ -120,6 +120,33 @@ def test_phong_scene_fused_render_and_unbounded_adjoint(oracle):
     P.close()
 
 
+def test_phong_sphere_bvh_instances(oracle, tmp_path):
+    """The SPEC x BVH kernel instances (a Phong material in a scene large
+    enough for the triangle BVH): the north-star scene with the sphere given
+    Ks 0.4, shininess 30.  Forward samples bit-exact (bounded and unbounded),
+    bounded and unbounded adjoints rtol 1e-9 against the oracle."""
+    from conftest import SCENE0
+
+    mtl = tmp_path / "shiny.mtl"
+    mtl.write_text("newmtl shiny\nKd 0.2 0.6 0.3\nKs 0.4 0.4 0.4\nNs 30\n")
+    src = open(SPHERE_OBJ).read()
+    i = src.index("\nf ") + 1
+    obj = tmp_path / "sphere_shiny.obj"
+    obj.write_text(src[:i] + "mtllib shiny.mtl\nusemtl shiny\n" + src[i:])
+    recs = SCENE0 + [((-1.2, -1.35, 4.6), (0, 0, 0), (1.2, 1.2, 1.2), str(obj), str(mtl))]
+    P, Q = product_scene(recs), oracle.OracleScene(recs)
+    assert P.nT > 1000 and np.any(P.triangles()[:, 28:31] > 0)
+    W, H, spp, seed = 32, 24, 8, 12
+    adj = np.random.RandomState(3).uniform(-1, 1, (H, W, 3)).astype(np.float32)
+    for mb in (4, None):
+        got = P.render_samples(W, H, spp, mb, seed)
+        want, _ = Q.render_samples(W, H, spp, mb, seed)
+        assert np.array_equal(bits(got), bits(want)), mb
+        np.testing.assert_allclose(P.adjoint(adj, W, H, spp, mb, seed), Q.adjoint(W, H, spp, mb, seed, adj),
+                                   rtol=1e-9, atol=1e-12, err_msg=str(mb))
+    P.close()
+
+
 def test_no_emitters_is_black_not_nan(oracle):
     recs = [((0, -1.5, 4), (0, 0, 0), (1, 1, 1), CUBE_OBJ, "*Kd 0.5 0.5 0.5*")]
     P, Q = product_scene(recs), oracle.OracleScene(recs)
