@@ -17,6 +17,7 @@
 #   valumix      VALU instruction-mix counter passes of the C2 headline
 #   uprof        kernel stats + FETCH/WRITE/TCC passes of the unbounded legs (tools/unbounded_prof.py)
 #   usq          SQ counter passes of the unbounded legs
+#   ulds / lds   LDS bank-conflict counters of the unbounded legs / the C2 headline
 #   nsprof       rocprofv3 --kernel-trace --stats of the north-star scene (BVH instances)
 #   nspmc        FETCH/WRITE + SQ counter passes of the north-star scene
 #   scenes       tools/bench_scenes.py ($SCENES, default all)
@@ -81,6 +82,8 @@ run() {
            SETS=$'FETCH_SIZE\nWRITE_SIZE\nTCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum' pmc_passes upmc "${UP[@]}" --steps 2 ;;
     valumix) SETS=$MIX_SETS pmc_passes valumix "${BENCHQ[@]}" ;;
     usq) SETS=$SQ_SETS pmc_passes usq "${UP[@]}" --steps 2 ;;
+    ulds) SETS="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAVE_CYCLES" pmc_passes ulds "${UP[@]}" --steps 2 ;;
+    lds) SETS="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAVE_CYCLES" pmc_passes lds "${BENCHQ[@]}" ;;
     nsprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/nsprof_$T" -o run --output-format csv \
                 -- "${NS[@]}" --steps 10 > "$OUT/nsprof_$T.log" 2>&1 ;;
     nspmc) SETS=$'FETCH_SIZE\nWRITE_SIZE\n'"$SQ_SETS" pmc_passes nspmc "${NS[@]}" --steps 2 ;;
