@@ -294,6 +294,55 @@ def _stream(hip):
     return raw, torch.cuda.ExternalStream(raw.value)
 
 
+@pytest.mark.parametrize("nstreams", [3, 4])
+def test_frames_in_flight_equal_frames_alone(nstreams):
+    """bench.py's headline form: consecutive C2 frames (per-step seeds) dealt
+    round-robin over `nstreams` fresh non-blocking streams, each stream with
+    its own image and gradient, no synchronisation between them -- the fused
+    render of every frame bitwise equal to the frame rendered alone, the
+    adjoint's fp64 gradient equal to the lone launch's to summation order."""
+    import torch
+
+    from inverse_path_tracer_amd import _native as N
+    from inverse_path_tracer_amd.distributed import frame_seed
+
+    L = N.lib()
+    hip = C.CDLL("libamdhip64.so")
+    sc = product_scene(CORNELL)
+    W = H = 128
+    spp, mb, frames = 64, 4, 9
+    ps = [N.make_params(W, H, spp, mb, frame_seed(0, i, W, H, spp)) for i in range(frames)]
+    adj = torch.full((H, W, 3), 1.0 / (3 * W * H), device="cuda")
+    streams = [_stream(hip) for _ in range(nstreams)]
+    try:
+        null = torch.cuda.current_stream().cuda_stream
+        alone_img, alone_g = [], []
+        for p in ps:
+            img = torch.empty((W * H, 3), device="cuda")
+            g = torch.zeros((sc.nT, 3), dtype=torch.float64, device="cuda")
+            N.check(L.ipt_render_dev(sc.handle, C.byref(p), None, img.data_ptr(), None, null))
+            N.check(L.ipt_adjoint_dev(sc.handle, C.byref(p), None, adj.data_ptr(), g.data_ptr(), null))
+            alone_img.append(img)
+            alone_g.append(g)
+        torch.cuda.synchronize()
+        imgs = [torch.full((W * H, 3), float("nan"), device="cuda") for _ in ps]
+        gs = [torch.zeros((sc.nT, 3), dtype=torch.float64, device="cuda") for _ in ps]
+        torch.cuda.synchronize()
+        for i, p in enumerate(ps):
+            st = streams[i % nstreams][1].cuda_stream
+            N.check(L.ipt_render_dev(sc.handle, C.byref(p), None, imgs[i].data_ptr(), None, st))
+            N.check(L.ipt_adjoint_dev(sc.handle, C.byref(p), None, adj.data_ptr(), gs[i].data_ptr(), st))
+        torch.cuda.synchronize()
+        for i in range(frames):
+            assert torch.equal(imgs[i].view(torch.int32), alone_img[i].view(torch.int32)), i
+            np.testing.assert_allclose(gs[i].cpu().numpy(), alone_g[i].cpu().numpy(), rtol=1e-12, atol=1e-18)
+    finally:
+        torch.cuda.synchronize()
+        sc.close()
+        for raw, _ in streams:
+            hip.hipStreamDestroy(raw)
+
+
 def test_mixed_launch_kinds_share_one_stream(scenes):
     """Every kind of launch may follow any other on a stream: single-set
     renders, 8-set scene batches (as many counter words as a single launch
