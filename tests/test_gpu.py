@@ -189,10 +189,12 @@ def test_row_band_sharding_bit_exact(scenes, W, H, spp, mb, world):
     # spp not a power of two (the weight division path), long paths (many sweep tasks per lane)
     ("scene0", 20, 12, 3, 5, 5), ("cornell", 24, 16, 5, 20, 7),
     # the reference's own estimator (no cap): ring records + chunk replays of paths longer than the ring
-    ("scene0", 64, 64, 8, None, 3), ("cornell", 33, 21, 16, None, 9)])
+    ("scene0", 64, 64, 8, None, 3), ("cornell", 33, 21, 16, None, 9),
+    # unbounded with spp not a power of two and a 64-bit seed
+    ("scene0", 19, 13, 7, None, 2**33 + 11)])
 def test_adjoint_matches_oracle(scenes, name, W, H, spp, mb, seed):
     P, Q = scenes[name]
-    adj = np.random.RandomState(seed).uniform(-1, 1, (H, W, 3)).astype(np.float32)
+    adj = np.random.RandomState(seed % 2**32).uniform(-1, 1, (H, W, 3)).astype(np.float32)
     g = P.adjoint(adj, W, H, spp, mb, seed)
     want = Q.adjoint(W, H, spp, mb, seed, adj)
     np.testing.assert_allclose(g, want, rtol=1e-9, atol=1e-12)
@@ -211,13 +213,14 @@ def test_adjoint_six_wave_instance_matches_oracle(scenes, monkeypatch, name, W, 
 
 
 def test_back_to_back_launches_with_ragged_chunks(scenes):
-    """Launches on one stream share the chunk counters, which the last wave of
-    each launch zeroes (ipt_hip.hip TraceArgs::ctr_done).  509 x 97 pixels:
+    """Launches on one stream share the chunk counters, which the launch's
+    last grab zeroes (ipt_hip.hip grab_failed, TraceArgs::grabs: the host's
+    count of the launch's grabs).  509 x 97 pixels:
     the fused render's last 8-pixel chunk holds 5 (more than its 4-pixel
     small chunk) and the adjoint's 789 968 samples leave 80 (more than 64)
     past the last full 128-item chunk, with more chunks than waves -- round
-    4's host-side count of the grabs had to match the kernel's enumeration
-    exactly, or every later launch re-traced a chunk."""
+    4's host-side count of the grabs (and round 5's) has to match the
+    kernel's enumeration exactly, or later launches skip or re-trace chunks."""
     P, Q = scenes["scene0"]
     W, H, spp, mb, seed = 509, 97, 16, 4, 21
     adj = np.random.RandomState(8).uniform(-1, 1, (H, W, 3)).astype(np.float32)
