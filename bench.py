@@ -157,12 +157,18 @@ def cpu_baseline(seconds_per_leg=1.5):
     from inverse_path_tracer_amd import png_read
     target = png_read(GRAPH_TARGET)
     out = {}
+    # every CPU in the affinity mask ("all host cores"), for
+    # the fast build's C2 forward and C3 adjoint -- the job's own share
+    # (OMP_NUM_THREADS, 16 on the GPU box) is the primary figure
+    allc = max(cores, affinity)
     for fast in (False, True):
         scenes = {k: oracle_lib.OracleScene(v, fast=fast) for k, v in recs.items()}
         L = oracle_lib.lib(fast)
-        for threads in (cores, 1):
+        for threads in ((cores, 1, allc) if fast and allc > cores else (cores, 1)):
             L.oro_set_threads(threads)
             for leg, (sc_name, w, h, spp, mb, kind) in legs.items():
+                if threads == allc and threads != cores and leg not in ("c2_fwd", "c3_adj"):
+                    continue
                 sc = scenes[sc_name]
                 adj = np.ones((h, w, 3), np.float32)
                 rows, row, total, secs = 2, 0, 0, 0.0
@@ -179,18 +185,29 @@ def cpu_baseline(seconds_per_leg=1.5):
                     total += r
                     row = (row + r) % h
                     rows *= 2
-                key = "%s_%s_%s" % (leg, "fast" if fast else "parity", "1core" if threads == 1 else "all")
-                out[key] = {"Msamples_s": round(total * w * spp / secs / 1e6, 3), "rows": total, "s": round(secs, 2)}
+                key = "%s_%s_%s" % (leg, "fast" if fast else "parity",
+                                    "1core" if threads == 1 else ("all" if threads == cores else "allcores"))
+                out[key] = {"Msamples_s": round(total * w * spp / secs / 1e6, 3), "rows": total, "s": round(secs, 2),
+                            "threads": threads}
         L.oro_set_threads(cores)
     c2 = out["c2_fwd_fast_all"]
-    return {"value": c2["Msamples_s"], "unit": "Msamples/s", "cores": cores, "kind": "port",
+    ac = {}
+    if "c2_fwd_fast_allcores" in out:
+        ac = {"value_allcores": out["c2_fwd_fast_allcores"]["Msamples_s"],
+              "grad_value_allcores": out["c3_adj_fast_allcores"]["Msamples_s"], "cores_allcores": allc}
+    else:  # the job's share is already every CPU it may use
+        ac = {"value_allcores": c2["Msamples_s"], "grad_value_allcores": out["c3_adj_fast_all"]["Msamples_s"],
+              "cores_allcores": cores}
+    return {"value": c2["Msamples_s"], "unit": "Msamples/s", "cores": cores, "kind": "port", **ac,
             "sample": "CPU oracle (oracle/ipt_oracle.c) fast build (-O3 x86-64-v3 -fopenmp) on %d rows of the "
                       "C2 frame (%.1f s); legs: C1/C2 forward and C3 adjoint, parity and fast builds, %d cores and "
                       "1 core, >= %.1f s each (table in `legs`)" % (c2["rows"], c2["s"], cores, seconds_per_leg),
             "grad_value": out["c3_adj_fast_all"]["Msamples_s"], "value_1core": out["c2_fwd_fast_1core"]["Msamples_s"],
             "graph_value": out["graph_fast_all"]["Msamples_s"],
             "cores_note": "%d = this job's CPU share (OMP_NUM_THREADS on the GPU box; %d CPUs in the affinity mask, "
-                          "%d in the machine)" % (cores, affinity, os.cpu_count() or 0),
+                          "%d in the machine); value_allcores / grad_value_allcores: the same fast-build C2 forward "
+                          "and C3 adjoint legs on all %d CPUs of the affinity mask"
+                          % (cores, affinity, os.cpu_count() or 0, allc),
             "legs": out}
 
 
@@ -453,6 +470,18 @@ def main():
     # host: there the adjoint steps stay on one stream)
     piped_adj = world == 1 or backend == "nccl"
     bwd_ms = cx.timed(lambda i: head.adjoint(i, piped=piped_adj), args.steps, head.streams if piped_adj else ())
+    # ... and the last NSTREAMS gradients in flight against the same adjoints
+    # alone on one stream: equal to fp64 summation order (the atomics' order)
+    gots = {i: head.grad2[i % len(head.streams)].clone() for i in last} if piped_adj else {}
+    adj_ok = []
+    for i in gots:
+        head.adjoint(i)
+        torch.cuda.synchronize()
+        g, w = gots[i].cpu().numpy(), head.grad.cpu().numpy()
+        adj_ok.append(bool(np.allclose(g, w, rtol=1e-9, atol=1e-12 * max(np.abs(w).max(), 1e-300))))
+    if not all(adj_ok):
+        print("bench: adjoints in flight differ from adjoints alone: %s" % adj_ok, file=sys.stderr)
+        bwd_ms = bwd_serial_ms
     frame = W * H * SPP
     value = args.steps * frame / (fwd_ms / 1e3) / 1e6
     grad_value = args.steps * frame / (bwd_ms / 1e3) / 1e6
@@ -465,7 +494,12 @@ def main():
              "piped_frames_bitwise_equal_alone": piped_ok,
              "headline_forward_form": ("%d frames in flight" % len(head.streams) if all(piped_ok) else
                                        "INVALID in flight (frames differed from frames rendered alone): "
-                                       "value is the one-stream rate")}
+                                       "value is the one-stream rate"),
+             "piped_gradients_equal_alone": adj_ok,
+             "headline_adjoint_form": (("%d adjoints in flight" % len(head.streams) if all(adj_ok) else
+                                        "INVALID in flight (gradients differed from adjoints alone beyond fp64 "
+                                        "summation order): grad_value is the one-stream rate")
+                                       if piped_adj else "one stream (gloo)")}
     if not args.no_secondary:
         # sustained rates (>= 0.5 s of back-to-back steps per leg; DVFS-steady)
         k, ms = cx.sustained(lambda i: head.fwd(i))

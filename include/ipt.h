@@ -155,7 +155,10 @@ int ipt_scene_shadow_masks(void *scene, uint32_t *masks);
  * (the BVH stops once the target is known to be occluded; small scenes use
  * the megakernel's culled shadow cast, which reports -1 when occluded);
  * < 0 a path ray through the megakernel's path cast (small scenes: the
- * culled pair loop).  Without targets small scenes run the full pair loop. */
+ * culled pair loop).  Without targets small scenes run the full pair loop.
+ * Directions need not be unit vectors (t is then in units of |dir|): the
+ * BVH's tree-entry culls that assume |dir| = 1, as the megakernel's rays
+ * have, are applied only to rays with |dot(dir, dir) - 1| <= 2^-20. */
 int ipt_closest_hit_host(void *scene, int64_t n, const float *origins, const float *dirs, const int32_t *targets,
                          float *t, int32_t *idx);
 int ipt_closest_hit_dev(void *scene, int64_t n, const float *origins_dev, const float *dirs_dev,

@@ -1080,14 +1080,17 @@ __device__ __forceinline__ float bperm_f(int addr, float v) {
 #ifndef IPT_TREE_SPHERE
 #define IPT_TREE_SPHERE 1
 #endif
-__device__ __forceinline__ bool coop_root_test(const CoopView &C, V3 p, V3 d, float bt) {
+// The sphere test (b^2 - cc with b = oc.d) and tree_skip's fixed dot margin
+// assume |d| = 1: the megakernel's rays come from unit().  `unit` false (a
+// caller's ray of any length, closest_hit_kernel) keeps the box test only.
+__device__ __forceinline__ bool coop_root_test(const CoopView &C, V3 p, V3 d, float bt, bool unit = true) {
   const SlabRay r = slab_ray(p, d);
   const float tx0 = fmaf(C.root[0], r.ix.x, r.ox.x), tx1 = fmaf(C.root[3], r.ix.x, r.ox.x);
   const float ty0 = fmaf(C.root[1], r.iy.x, r.oy.x), ty1 = fmaf(C.root[4], r.iy.x, r.oy.x);
   const float tz0 = fmaf(C.root[2], r.iz.x, r.oz.x), tz1 = fmaf(C.root[5], r.iz.x, r.oz.x);
   const float en = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.f));
   const float ex = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), bt));
-  if (IPT_TREE_SPHERE) {
+  if (IPT_TREE_SPHERE && unit) {
     const V3 oc = mk(p.x - C.sphere[0], p.y - C.sphere[1], p.z - C.sphere[2]);
     const float b = dot3(oc, d), cc = dot3(oc, oc) - C.sphere[3];
     const bool miss = cc > 0.f && (b > 0.f || fmaf(b, b, -cc) < 0.f);
@@ -1102,8 +1105,8 @@ __device__ __forceinline__ bool coop_root_test(const CoopView &C, V3 p, V3 d, fl
 #ifndef IPT_TREE_SKIP
 #define IPT_TREE_SKIP 1
 #endif
-__device__ __forceinline__ bool tree_skip(const float4 *sc, int s, V3 d) {
-  if (s < 0) return false;
+__device__ __forceinline__ bool tree_skip(const float4 *sc, int s, V3 d, bool unit = true) {
+  if (s < 0 || !unit) return false;
   const float4 v = sc[s];
   return dot3(mk(v.x, v.y, v.z), d) >= v.w;
 }

@@ -1937,6 +1937,10 @@ struct GpuScene {
     uint32_t *dev;
   };
   std::vector<Counters> counters;
+  // buffers a grow replaced: a launch on another host thread may hold one it
+  // took before the grow and not have enqueued its kernel yet, so they live
+  // until gpu_free
+  std::vector<uint32_t *> counters_retired;
   std::mutex counters_mu;
 };
 
@@ -2074,6 +2078,7 @@ void gpu_free(GpuScene *s) {
   (void)hipFree(s->grad_map);
   (void)hipFree(s->slot_tri);
   for (auto &c : s->counters) (void)hipFree(c.dev);
+  for (uint32_t *p : s->counters_retired) (void)hipFree(p);
   delete s;
 }
 
@@ -2291,8 +2296,11 @@ struct StreamScratch {
 
 // The chunk counters of launches on stream `st` with `words` grab words:
 // one buffer per (scene, stream), allocated and zeroed (on `st`, in stream
-// order) at the stream's first launch and grown when a launch needs more
-// words.  Every launch leaves them zeroed
+// order) at the stream's first launch and replaced by a larger one when a
+// launch needs more words (the old one is kept until gpu_free: another host
+// thread may have taken it for a launch it has not enqueued yet -- launches
+// already queued on it leave it zeroed and never touch the new one, so no
+// synchronisation is needed).  Every launch leaves them zeroed
 // (TraceArgs::chunk_ctr), so the host keeps no copy of device state: a launch
 // that fails before or after enqueueing changes nothing the next one depends
 // on, and any kind of launch (single set, regions, scene batch) may follow any
@@ -2314,9 +2322,8 @@ static int stream_counters(GpuScene *s, hipStream_t st, int words, uint32_t **ou
   GpuScene::Counters *c = nullptr;
   for (auto &e : s->counters)
     if (e.stream == st) c = &e;
-  if (c && c->words < words) {  // grow (after the launches queued on the old buffer)
-    HIP_TRY(hipStreamSynchronize(st));
-    HIP_TRY(hipFree(c->dev));
+  if (c && c->words < words) {  // grow: a new buffer; the old one is retired, not freed
+    s->counters_retired.push_back(c->dev);
     c->dev = nullptr;
     c->words = 0;
   }
@@ -2750,14 +2757,18 @@ int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const f
       }
       nl = s->adju_nl;
     }
-    // (>= 1: a lane's first record never waits for a pool chunk; launch_inst
+    // (>= 1: a lane's first record never waits for a pool chunk -- with none
+    // left it could not start its ring -- so a scene whose LDS base leaves no
+    // room for one slot at full residency runs with one workgroup less; one
+    // that leaves no room for one slot at all is refused below; launch_inst
     // sizes the global part)
     if (g_adju_lds.load() > 0) nl = g_adju_lds.load();
     a.rec_lds = std::max(1, std::min(nl, kAdjuRing - 1));
   }
   const size_t lds = base + (size_t)(unbounded ? a.rec_lds : a.rec_cap) * fields * kBlock * sizeof(float);
   if (lds > 160 * 1024) {
-    gpu_set_error("adjoint LDS footprint exceeds 160 KiB; lower max_bounces");
+    gpu_set_error(unbounded ? "unbounded adjoint: the scene's LDS tables plus one record slot per lane exceed 160 KiB"
+                            : "adjoint LDS footprint exceeds 160 KiB; lower max_bounces");
     return -1;
   }
   if (unbounded)
@@ -2998,13 +3009,17 @@ __global__ __launch_bounds__(kBlock) void closest_hit_kernel(const TriIsect *__r
   if (BVH) {
     bool qn = false;
     if (valid) {
+      // the tree-entry culls (sphere, source plane) hold for the megakernel's
+      // unit directions; a caller's ray of another length takes the box test
+      // only, so the BVH answers the brute-force loop for any direction
+      const bool unit = fabsf(dot3(d, d) - 1.f) <= 0x1p-20f;
       if (target >= 0) {
         const uint32_t allow = probe_allow(IPT_SHADOW_PO ? a.big_pomask : nullptr, emit_tri, a.nE, nT, src, target);
         if (bvh_prepass<true>(bv, p, d, t, h, target, allow))
-          qn = coop_root_test(cv, p, d, t) && !(IPT_TREE_SKIP && tree_skip(a.src_cull, src, d));
+          qn = coop_root_test(cv, p, d, t, unit) && !(IPT_TREE_SKIP && tree_skip(a.src_cull, src, d, unit));
       } else {  // (a path ray with a source: the megakernel's bounce ray leaving that triangle)
         bvh_prepass<false>(bv, p, d, t, h, -1);
-        qn = coop_root_test(cv, p, d, t) && !(IPT_TREE_SKIP && tree_skip(a.src_cull, src, d));
+        qn = coop_root_test(cv, p, d, t, unit) && !(IPT_TREE_SKIP && tree_skip(a.src_cull, src, d, unit));
       }
     }
     coop_cast<false>(cv, qn && target < 0, p, d, t, h);

@@ -417,6 +417,76 @@ def test_mixed_launch_kinds_share_one_stream(scenes):
             hip.hipStreamDestroy(raw)
 
 
+def test_counter_grow_with_concurrent_launches_on_one_stream(scenes):
+    """The chunk-counter buffer of a (scene, stream) is replaced by a larger
+    one when a launch needs more words than it has (a scene batch of more
+    than 16 sets).  Two host threads launch on ONE stream at once -- single
+    renders and 20-set batches (ctypes releases the GIL, so the calls
+    interleave) -- after a single render sized the buffer at 16 words: the
+    replaced buffer stays alive for launches that took it before the grow
+    (ADVICE r5), and every result equals the same launch alone."""
+    import threading
+
+    import torch
+
+    from inverse_path_tracer_amd import _native as N
+
+    L = N.lib()
+    hip = C.CDLL("libamdhip64.so")
+    P = product_scene(SCENE0)
+    W, H, spp, mb, seed = 64, 48, 16, 4, 19
+    S, stride = 20, W * H * spp
+    kd = torch.from_numpy(np.random.RandomState(8).uniform(0, 1, (S, P.nT, 3)).astype(np.float32)).cuda()
+    p = N.make_params(W, H, spp, mb, seed)
+    raws = []
+    try:
+        def single(st):
+            o = torch.empty((H * W, 3), device="cuda")
+            N.check(L.ipt_render_dev(P.handle, C.byref(p), kd[5].data_ptr(), o.data_ptr(), None, st))
+            return o
+
+        def batch(st):
+            o = torch.empty((S, H * W, 3), device="cuda")
+            N.check(L.ipt_render_batch_dev(P.handle, C.byref(p), S, stride, kd.data_ptr(), o.data_ptr(), st))
+            return o
+
+        raw, st = _stream(hip)
+        raws.append(raw)
+        want_single, want_batch = single(st.cuda_stream), batch(st.cuda_stream)
+        torch.cuda.synchronize()
+        raw, st = _stream(hip)
+        raws.append(raw)
+        s = st.cuda_stream
+        first = single(s)  # sizes this stream's counters at 16 words
+        outs = {"a": [], "b": []}
+        errs = []
+
+        def worker(key, fn, n):
+            try:
+                for _ in range(n):
+                    outs[key].append(fn(s))
+            except Exception as e:  # noqa: BLE001 (re-raised below)
+                errs.append(e)
+
+        ths = [threading.Thread(target=worker, args=("a", single, 8)),
+               threading.Thread(target=worker, args=("b", batch, 3))]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        torch.cuda.synchronize()
+        assert not errs, errs
+        for o in [first] + outs["a"]:
+            assert torch.equal(o.view(torch.int32), want_single.view(torch.int32))
+        for o in outs["b"]:
+            assert torch.equal(o.view(torch.int32), want_batch.view(torch.int32))
+    finally:
+        torch.cuda.synchronize()
+        P.close()
+        for raw in raws:
+            hip.hipStreamDestroy(raw)
+
+
 def test_counter_reset_over_launch_shapes(scenes, oracle):
     """The chunk counters reset themselves only if the host's count of a
     launch's grabs (ipt_hip.hip launch_grabs) equals what the kernel's waves
@@ -1084,6 +1154,59 @@ def test_tree_entry_culls_equal_brute_force(which):
     vis_c, vis_f = ic == tgs, i_f == tgs
     assert np.array_equal(vis_c, vis_f)
     assert np.array_equal(bits(tc[vis_c]), bits(tf[vis_f]))
+    P.close()
+
+
+@pytest.mark.parametrize("scale", [0.5, 3.0])
+@pytest.mark.parametrize("which", ["northstar", "clutter", "scene0"])
+def test_closest_hit_with_non_unit_directions(which, scale):
+    """ipt_closest_hit / ipt_shadow_hit take caller directions of any length
+    (ADVICE r5): the BVH scenes' tree-entry culls assume |d| = 1 (the
+    megakernel's rays), so for other lengths the cast keeps only the box test
+    and still returns the brute-force loop's hit bit-for-bit; small scenes'
+    culled path cast likewise.  Rays from points on every triangle in all
+    directions (with their source triangle) and rays from the room at the
+    objects, directions scaled by 0.5 and 3."""
+    from inverse_path_tracer_amd import _native as N
+    from conftest import NORTHSTAR
+    from test_bvh import CLUTTER_SCENE
+
+    P = product_scene({"northstar": NORTHSTAR, "clutter": CLUTTER_SCENE, "scene0": SCENE0}[which])
+    tris = P.triangles()
+    v = tris[:, 0:9].reshape(-1, 3, 3).astype(np.float64)
+    rng = np.random.RandomState(53)
+    n = 200000
+    src = rng.randint(0, P.nT, n)
+    a, b = rng.uniform(0, 1, (2, n))
+    flip = a + b > 1
+    a[flip], b[flip] = 1 - a[flip], 1 - b[flip]
+    O = v[src, 0] + a[:, None] * (v[src, 1] - v[src, 0]) + b[:, None] * (v[src, 2] - v[src, 0])
+    D = rng.normal(size=(n, 3))
+    m = 100000
+    box = v.reshape(-1, 3)
+    Or = rng.uniform(box.min(0), box.max(0), (m, 3))
+    k = rng.randint(min(18, P.nT - 1), P.nT, m)
+    Dr = v[k].mean(1) + rng.normal(0, 0.03, (m, 3)) - Or
+    O = np.concatenate([O, Or]).astype(np.float32)
+    D = np.concatenate([D, Dr])
+    D = (D / np.linalg.norm(D, axis=1, keepdims=True) * scale).astype(np.float32)
+    S = np.concatenate([src, np.full(m, -1)]).astype(np.int32)
+    tg = np.full(len(O), -1, np.int32)
+    if P.bvh_info()["accel"] == "bvh":
+        tc, ic = P.shadow_hit(O, D, tg, S)  # the megakernel's path cast with its source triangle
+        P.set_accel(N.ACCEL_BVH)
+        tb, ib = P.closest_hit(O, D)
+        P.set_accel(N.ACCEL_BRUTE)
+        tf, i_f = P.closest_hit(O, D)
+        P.set_accel(N.ACCEL_AUTO)
+        assert np.array_equal(ib, i_f)
+        assert np.array_equal(bits(tb), bits(tf))
+    else:
+        tc, ic = P.closest_hit(O, D, targets=tg)  # the culled path cast
+        tf, i_f = P.closest_hit(O, D)
+    assert np.array_equal(ic, i_f)
+    assert np.array_equal(bits(tc), bits(tf))
+    assert (i_f >= 0).mean() > 0.4
     P.close()
 
 

@@ -88,6 +88,51 @@ def test_northstar_adjoint_matches_oracle(northstar, mb):
     np.testing.assert_allclose(g, want, rtol=1e-9, atol=1e-12 * np.abs(want).max())
 
 
+@pytest.mark.parametrize("mb", [4, None], ids=["4bounces", "unbounded"])
+def test_northstar_adjoint_c2_band_matches_oracle(northstar, mb):
+    """The adjoint at the size the bench times (c3_northstar /
+    c3_northstar_unbounded: 512x512, 64 spp): rows 344..359 (524 288 samples,
+    across the sphere and the cube) against the oracle's adjoint of the same
+    rows (path_trace.cu:166-183 differentiated; unbounded = the reference's
+    own estimator).  The grid is the same persistent grid as the full frame's
+    -- the resident workgroups of the BVH instance, 4 waves/SIMD for the
+    unbounded one, its per-wave pools of 63 chunks sized for that grid, the
+    band's ~1 chunk per wave -- so the launch shapes the bench credits run
+    here, pinned at rtol 1e-9 (fp64 sums; only the order differs)."""
+    P, Q = northstar
+    W = H = 512
+    spp, r0, r1 = 64, 344, 360
+    adj = np.random.RandomState(12).uniform(-1, 1, (H, W, 3)).astype(np.float32)
+    g = P.adjoint(adj, W, H, spp, mb, 0, r0, r1)
+    want = Q.adjoint(W, H, spp, mb, 0, adj, r0, r1)
+    assert np.abs(want[30:]).max() > 0
+    np.testing.assert_allclose(g, want, rtol=1e-9, atol=1e-12 * np.abs(want).max())
+
+
+def test_northstar_unbounded_adjoint_full_frame_properties(northstar):
+    """The benched launch itself (512x512x64, unbounded, 1310 triangles), whose
+    oracle run would take minutes: (1) linear in the adjoint image -- 2*a
+    gives exactly twice the gradient (a power of two scales every product
+    exactly) and a + b the sum at fp32 rounding of the image; (2) the sum of
+    the 8 interleaved row shares (bench.py's tile split, rows r, r+8, ...)
+    equals the full frame at fp64 summation order."""
+    P, _ = northstar
+    W = H = 512
+    spp = 64
+    rng = np.random.RandomState(21)
+    a = rng.uniform(-1, 1, (H, W, 3)).astype(np.float32)
+    b = rng.uniform(-1, 1, (H, W, 3)).astype(np.float32)
+    ga = P.adjoint(a, W, H, spp, None, 0)
+    scale = np.abs(ga).max()
+    assert np.abs(ga[30:]).max() > 0
+    np.testing.assert_allclose(P.adjoint(2 * a, W, H, spp, None, 0), 2 * ga, rtol=1e-10, atol=1e-10 * scale)
+    gb = P.adjoint(b, W, H, spp, None, 0)
+    gab = P.adjoint(a + b, W, H, spp, None, 0)
+    np.testing.assert_allclose(gab, ga + gb, rtol=1e-5, atol=1e-5 * max(scale, np.abs(gb).max()))
+    parts = sum(P.adjoint(a, W, H, spp, None, 0, r, H, row_step=8) for r in range(8))
+    np.testing.assert_allclose(parts, ga, rtol=1e-10, atol=1e-10 * scale)
+
+
 def test_northstar_graph_matches_oracle(northstar):
     """createGraph (inv_path_trace.cu:152-208) through the BVH: unbounded
     paths, a random 8-bit target image."""

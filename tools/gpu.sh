@@ -10,6 +10,7 @@
 #   tests        pytest -m gpu ($TESTS, default tests; $PYTEST_K for -k)
 #   bench        bench.py (full JSON line)
 #   benchq       bench.py --no-secondary --no-cpu-baseline
+#   benchd       bench.py exactly as the driver runs it (--gpus 1 --steps 20 --warmup 5)
 #   prof         rocprofv3 --kernel-trace --stats of the C2 headline (no secondary lines)
 #   pmc          FETCH_SIZE / WRITE_SIZE passes of the C2 headline (separate runs)
 #   sq           SQ counter passes of the C2 headline
@@ -71,6 +72,7 @@ run() {
     tests) timeout -k 10 1000 python -u -m pytest ${TESTS:-tests} -m gpu -v --maxfail=5 --timeout 300 \
                --timeout-method thread -p no:cacheprovider ${PYTEST_K:+-k "$PYTEST_K"} > "$OUT/pytest_gpu_$T.log" 2>&1 ;;
     bench) timeout -k 10 600 python bench.py > "$OUT/bench_$T.json" 2> "$OUT/bench_$T.err" ;;
+    benchd) timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/benchd_$T.json" 2> "$OUT/benchd_$T.err" ;;
     benchq) timeout -k 10 300 python bench.py --no-secondary --no-cpu-baseline > "$OUT/benchq_$T.json" 2> "$OUT/benchq_$T.err" ;;
     prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$T" -o run --output-format csv \
               -- python3 "$R/bench.py" --steps 20 --warmup 2 --no-cpu-baseline --no-secondary > "$OUT/prof_$T.log" 2>&1 ;;
