@@ -487,6 +487,9 @@ __device__ __forceinline__ void item_ray(const TraceArgs &a, uint64_t seed, uint
 #ifndef IPT_MIN_BLOCKS_ADJW
 #define IPT_MIN_BLOCKS_ADJW 6
 #endif
+#ifndef IPT_ADJW_LANE_LDS  // MODE_ADJW's work item and Le in LDS (trace_kernel's lane_ws)
+#define IPT_ADJW_LANE_LDS 1
+#endif
 #ifndef IPT_MIN_BLOCKS_GRAPH
 #define IPT_MIN_BLOCKS_GRAPH 0
 #endif
@@ -796,8 +799,14 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   // words: item lo, hi, source, Le xyz) instead of registers -- each is
   // touched a few times per path, and in registers the allocator spilled them
   // (and more) to scratch inside the loop
-  constexpr bool kLaneLds = BVH && is_fwd<MODE>();
+  // The 6-wave adjoint (MODE_ADJW, 80 VGPRs) likewise keeps its work item
+  // and Le there (its path source is not needed): in registers they pushed
+  // the culled path cast past 80 VGPRs and a ray-direction pair was reloaded
+  // from scratch in every pair block (16 B/lane of scratch; IPT_ADJW_LANE_LDS)
+  constexpr bool kLaneLds = (BVH && is_fwd<MODE>()) || (!BVH && MODE == MODE_ADJW && IPT_ADJW_LANE_LDS);
   lds_u32 *lane_ws = nullptr;
+  if (!BVH && kLaneLds)  // after the vertex records ([6][kBlock] words, as the BVH forward's)
+    lane_ws = (lds_u32 *)(lds_rec + (size_t)vmax * kRecFieldsDiffuse * kBlock);
   CoopView cv;
   cv.wn = nullptr;
   cv.wn_lds = false;
@@ -960,7 +969,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     if (kLaneLds) return (uint64_t)lane_ws[tid] | ((uint64_t)lane_ws[kBlock + tid] << 32);
     return witem_r;
   };
-  auto set_ptri = [&](int t) {
+  auto set_ptri = [&](int t) {  // (read by the BVH instances' tree_skip only)
+    if (!BVH) return;
     if (kLaneLds) lane_ws[2 * kBlock + tid] = (uint32_t)t;
     else ptri_r = t;
   };
@@ -2775,11 +2785,13 @@ int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const f
     return launch<MODE_ADJU>(s, a, lds, kd_dev, nullptr, adj_dev, grad_dev, nullptr, nullptr, (hipStream_t)stream);
   // the 6-wave instance for full-size launches whose LDS leaves room for a
   // sixth workgroup per CU (IPT_ADJW=0/1 in the environment forces the choice)
-  bool wide = !use_bvh(s) && !s->has_ks && 6 * lds <= 160 * 1024 &&
+  const size_t lane_words = IPT_ADJW_LANE_LDS ? (size_t)6 * kBlock * sizeof(uint32_t) : 0;  // trace_kernel's lane_ws
+  bool wide = !use_bvh(s) && !s->has_ks && 6 * (lds + lane_words) <= 160 * 1024 &&
               (uint64_t)a.n_samples * (uint64_t)std::max(1, a.nscenes) >= IPT_ADJW_MIN_SAMPLES;
   if (const char *e = std::getenv("IPT_ADJW")) wide = std::atoi(e) != 0 && !use_bvh(s) && !s->has_ks;
   if (wide)
-    return launch<MODE_ADJW>(s, a, lds, kd_dev, nullptr, adj_dev, grad_dev, nullptr, nullptr, (hipStream_t)stream);
+    return launch<MODE_ADJW>(s, a, lds + lane_words, kd_dev, nullptr, adj_dev, grad_dev, nullptr, nullptr,
+                             (hipStream_t)stream);
   return launch<MODE_ADJ>(s, a, lds, kd_dev, nullptr, adj_dev, grad_dev, nullptr, nullptr, (hipStream_t)stream);
 }
 

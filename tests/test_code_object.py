@@ -28,7 +28,8 @@ BUDGET = {
     (0, False, False): 0,   # forward (sample buffer)
     (4, False, False): 0,   # fused render: the C2 headline
     (1, False, False): 0,   # adjoint: the C2 headline's gradient
-    (5, False, False): 16,  # adjoint at 6 waves/SIMD (80 VGPRs, full-size launches): 3 spilled VGPRs
+    (5, False, False): 8,   # adjoint at 6 waves/SIMD (80 VGPRs, full-size launches): work item + Le in LDS, one
+                            # loop-invariant word spilled before the loop (round 5: 16 B, reloaded per pair block)
     (2, False, False): 0,   # createGraph
     (2, False, True): 0,
     (1, False, True): 0,    # BVH adjoint (2 waves/SIMD, 256 VGPRs allowed)

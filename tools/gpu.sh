@@ -32,6 +32,9 @@
 #   workflow     tools/workflow_at_size.py (pipeline all --n 100 + optimize --n 100)
 #   graphprof    rocprofv3 --kernel-trace --stats of createGraph at the reference config (tools/graph_prof.py)
 #   pipeab       tools/pipeline_ab.py (consecutive frames on one stream vs two)
+#   adjpmc       tools/adj_pmc.py: kernel stats + FETCH/WRITE/TCC/TCP passes of the C2 fused render and adjoint,
+#                for the default library, $ADJ_VARIANT (a lib/variants build) and the 5-wave adjoint (IPT_ADJW=0)
+#   counters     rocprofv3 -L (the counters this box offers)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 R=$(pwd)
@@ -104,6 +107,19 @@ run() {
     workflow) timeout -k 10 1000 python -u tools/workflow_at_size.py --out "$OUT/workflow_$T.json" > "$OUT/workflow_$T.log" 2>&1 ;;
     graphprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/graphprof_$T" -o run --output-format csv \
                    -- python3 "$R/tools/graph_prof.py" --steps 20 > "$OUT/graphprof_$T.log" 2>&1 ;;
+    adjpmc) local sets=$'FETCH_SIZE\nWRITE_SIZE\nTCC_EA0_WRREQ_sum TCC_EA0_ATOMIC_sum TCC_EA0_RDREQ_sum TCC_MISS_sum\nTCP_TCC_WRITE_REQ_sum TCP_TCC_READ_REQ_sum TCP_TCC_ATOMIC_WITHOUT_RET_REQ_sum TCP_TCC_ATOMIC_WITH_RET_REQ_sum'
+            timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/adjstats_$T" -o run --output-format csv \
+                -- python3 "$R/tools/adj_pmc.py" --steps 10 > "$OUT/adjstats_$T.log" 2>&1 &&
+            SETS=$sets pmc_passes adjpmc_new python3 "$R/tools/adj_pmc.py" &&
+            ( export IPT_ADJW=0; SETS=$sets pmc_passes adjpmc_five python3 "$R/tools/adj_pmc.py" --no-fwd ) &&
+            if [ -n "$ADJ_VARIANT" ]; then
+              ( export IPT_AMD_LIB=$R/inverse_path_tracer_amd/lib/variants/libipt_$ADJ_VARIANT.so
+                SETS=$sets pmc_passes adjpmc_var python3 "$R/tools/adj_pmc.py" ) &&
+              ( export IPT_AMD_LIB=$R/inverse_path_tracer_amd/lib/variants/libipt_$ADJ_VARIANT.so
+                timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/adjstats_var_$T" -o run --output-format csv \
+                    -- python3 "$R/tools/adj_pmc.py" --steps 10 > "$OUT/adjstats_var_$T.log" 2>&1 )
+            fi ;;
+    counters) timeout -k 10 120 rocprofv3 -L > "$OUT/counters_$T.txt" 2>&1 ;;
     pipeab) timeout -k 10 300 python tools/pipeline_ab.py > "$OUT/pipeab_$T.log" 2>&1 ;;
     *) echo "unknown stage $1" >&2; return 2 ;;
   esac
