@@ -565,8 +565,23 @@ constexpr int min_blocks() {
 // accumulates s_memtime cycles per phase of the loop; read with
 // ipt_debug_phase_cycles (tools/phase_timing.py).
 #ifdef IPT_PHASE_TIMING
-__device__ unsigned long long g_phase_cycles[10];
-// [8], [9]: the tree (coop_cast) part of phases 1 and 3 (BVH scenes)
+constexpr int kPhaseWords = 26;
+__device__ unsigned long long g_phase_cycles[kPhaseWords];
+// [8], [9]: the tree (coop_cast) part of phases 1 and 3 (BVH scenes);
+// [10..21]: per phase, the lanes that take part summed over the wave
+// iterations that run it, and those iterations (PHASE_LANES): refill,
+// shade, shadow cast, emitter term, finalise, adjoint sweep rounds (valid
+// tasks per round); [22] the sweep's chain steps (wave-level), [23] the
+// rounds that run a chain, [24] the lanes' own chain steps summed (the
+// useful part of [22] x 64); the path cast's lanes are [7]
+#define PHASE_LANES(i, cond)                             \
+  {                                                      \
+    const uint64_t b_ = __ballot(cond);                  \
+    if (b_) {                                            \
+      tacc[i] += (uint64_t)__popcll(b_);                 \
+      tacc[(i) + 1] += 1;                                \
+    }                                                    \
+  }
 #define SUBPHASE_BEGIN const uint64_t ts_ = __builtin_amdgcn_s_memtime();
 #define SUBPHASE_END(i) tacc[i] += __builtin_amdgcn_s_memtime() - ts_;
 #define PHASE(i)                                     \
@@ -579,6 +594,7 @@ __device__ unsigned long long g_phase_cycles[10];
 #define PHASE(i)
 #define SUBPHASE_BEGIN
 #define SUBPHASE_END(i)
+#define PHASE_LANES(i, cond)
 #endif
 
 // Path ray of the brute-force scenes: the unrolled pair loop with plane
@@ -984,7 +1000,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   // block thus runs once per vertex with most lanes on, instead of path and
   // shadow lanes serialising each other's code every iteration.
 #ifdef IPT_PHASE_TIMING
-  uint64_t tacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t tacc[kPhaseWords] = {};
   uint64_t tp_ = __builtin_amdgcn_s_memtime();
 #endif
   const int lane = tid & 63;
@@ -1123,6 +1139,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     }
     // ---- refill finished lanes from the wave's range (ballot + mbcnt)
     const uint64_t need = __ballot(!active);
+#ifdef IPT_PHASE_TIMING
+    const uint64_t act0_ = ~need;
+#endif
     if (MODE == MODE_FWDM) {
       const uint32_t fn = gnp * (uint32_t)a.spp;
       if (need && fj < fn) {
@@ -1180,6 +1199,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       next += (uint64_t)__popcll(need);
     }
     PHASE(0)
+    PHASE_LANES(10, active && !((act0_ >> (tid & 63)) & 1ull))
     // (MODE_FWDM: the last finished slots are summed at the loop top first)
     if (__ballot(active) == 0 && (MODE != MODE_FWDM || (exhausted && sdone == 0 && fj >= gnp * (uint32_t)a.spp)))
       break;
@@ -1294,6 +1314,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
 
     // ================= phase 2: next-event shadow ray (path_trace.cu:73-88)
     PHASE(2)
+    PHASE_LANES(12, vertex)
     V3 lo = mk(0.f, 0.f, 0.f);
     float emit_s = 0.f;  // ADJ record: lo = Ke[emit_et] * emit_s
     int emit_et = 0;
@@ -1301,6 +1322,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     int hs = -1;
     const int et = shadow ? emit_tri[emitter] : -1;
     if (__ballot(shadow)) {
+      PHASE_LANES(14, shadow)
       if (BVH) {
         bool qn = false;
         if (shadow && bvh_prepass<true>(bv, p, sd, ts, hs, et,
@@ -1368,6 +1390,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     }
 
     PHASE(4)
+    PHASE_LANES(16, shadow && hs == et)
     if (MODE == MODE_ADJU) {
       // a lane about to write the first slot of a pool chunk it does not hold
       // takes one (wave-uniform hand-out in lane order); none left: the ring
@@ -1397,6 +1420,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       }
     }
     // ================= finalise the vertex
+    PHASE_LANES(18, vertex)
     if (vertex) {
       if (is_badj<MODE>()) {  // vertex record k (layout [field][vertex][lane])
         float *rec = lds_rec + (size_t)k * kBlock + tid;
@@ -1566,6 +1590,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           const int next = __builtin_amdgcn_readlane(inc, 63 - (int)__builtin_clzll(fit));
           const int t = base + lane;
           const bool valid = t < next;
+          PHASE_LANES(20, valid)
           // owners of this round mark their first task's lane with (start,
           // first pass, escaped, K, owner lane) + 1 -- start in the top bits,
           // so an inclusive max-scan leaves every task lane the marker of the
@@ -1717,6 +1742,11 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             }
             Mk = mk(mx, my, mz);
             S = mk(sx, sy, sz);
+#ifdef IPT_PHASE_TIMING
+            tacc[22] += (uint64_t)(s - 1);  // chain steps of this round (s: one past the last)
+            tacc[23] += 1;
+            tacc[24] += (uint64_t)__builtin_amdgcn_readlane(wave_scan_add(steps), 63);
+#endif
           }
           // (the owner's adjoint weights are taken only here: their global
           // loads, issued as the sweep starts, finish under the chain)
@@ -1784,7 +1814,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   }
 #ifdef IPT_PHASE_TIMING
   if ((tid & 63) == 0)
-    for (int i = 0; i < 10; ++i) atomicAdd(&g_phase_cycles[i], (unsigned long long)tacc[i]);
+    for (int i = 0; i < kPhaseWords; ++i) atomicAdd(&g_phase_cycles[i], (unsigned long long)tacc[i]);
 #endif
   }
 
@@ -1955,9 +1985,10 @@ struct GpuScene {
 };
 
 #ifdef IPT_PHASE_TIMING
-extern "C" int ipt_debug_phase_cycles(unsigned long long *out) {  // read and reset
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), 10 * sizeof(unsigned long long)) != hipSuccess) return -1;
-  unsigned long long z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+extern "C" int ipt_debug_phase_cycles(unsigned long long *out) {  // read and reset (kPhaseWords words)
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), kPhaseWords * sizeof(unsigned long long)) != hipSuccess)
+    return -1;
+  unsigned long long z[kPhaseWords] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof z) == hipSuccess ? 0 : -1;
 }
 #endif
