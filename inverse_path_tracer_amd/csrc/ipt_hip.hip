@@ -189,6 +189,19 @@ constexpr int kPoolSlots = 16, kPoolMaxChunks = 4;
 #define IPT_ADJU_LDS_SLOTS_FIXED -1
 #endif
 constexpr int kAdjuRing = IPT_ADJU_RING;
+// Sub-chunked sweep of the unbounded adjoint (IPT_ADJU_SUB = G > 0): a chunk
+// is swept G vertices at a time from its end, one sub-chunk per loop
+// iteration, the lane tracing nothing meanwhile (its suffix carried in Scar,
+// as between chunks), so a sweep round's chain runs at most G - 1 steps
+// instead of as long as the round's longest path.  The forward's M at every
+// G-th slot of a chunk (k > 0) is captured to a per-lane global array
+// (TraceArgs::mring, kMrEnt entries), which also replaces the chunk's Mlo
+// register.  0: whole chunks per round (round 5).
+#ifndef IPT_ADJU_SUB
+#define IPT_ADJU_SUB 0
+#endif
+constexpr int kSub = IPT_ADJU_SUB;
+constexpr int kMrEnt = kSub > 0 ? (kAdjuRing + kSub - 1) / kSub : 1;
 // Dynamic work distribution across the waves of a launch (TraceArgs::chunk):
 // static per-wave ranges left each launch's tail to the waves whose pixels
 // hold the longest paths -- C2 forward 2.41 -> 2.11 ms, sphere 6.61 -> 4.63 ms,
@@ -286,6 +299,9 @@ struct TraceArgs {
   float *grec;
   uint64_t grec_stride;
   int pool_chunks;  // ADJU: chunks per wave pool (<= 63)
+  // ADJU with IPT_ADJU_SUB: per wave [kMrEnt][64 lanes][3] floats, entry e
+  // = the forward's M before the update of the vertex in ring slot e * kSub
+  float *mring;
   // scene batch (C5): blocks b, b + nscenes, ... (bps of them) trace material
   // set b -- interleaved, not contiguous ranges: the dispatcher fills a CU
   // with consecutive workgroups, so contiguous ranges gave some sets fewer
@@ -890,6 +906,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   gbl_f32 *upool = nullptr;  // this wave's chunk pool ([chunk][slot][field])
   if (MODE == MODE_ADJU)
     upool = (gbl_f32 *)a.grec + ((size_t)blockIdx.x * (kBlock / 64) + (tid >> 6)) * a.grec_stride;
+  gbl_f32 *umr = nullptr;  // this lane's captured prefix throughputs (IPT_ADJU_SUB), entry e at umr + e * 192
+  if (MODE == MODE_ADJU && kSub > 0)
+    umr = (gbl_f32 *)a.mring + ((size_t)blockIdx.x * (kBlock / 64) + (tid >> 6)) * (kMrEnt * 64 * 3) + (tid & 63) * 3;
   {  // the wave's persistent loop
   // wave-uniform sample range (static partition, regenerated per lane)
   // XCD region (TraceArgs::nreg) of this block, and the wave's index among
@@ -961,6 +980,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   // starting at vertex 0; captured while a replay passes its start)
   V3 Scar = mk(0.f, 0.f, 0.f), Mlo = mk(1.f, 1.f, 1.f);
   int rhi = 0, rslot = 0;
+  // IPT_ADJU_SUB: the end of the sub-chunk this lane sweeps next (0: none);
+  // such a lane is neither traced nor refilled until its chunk is swept
+  int usub = 0;
+  auto pending = [&]() { return MODE == MODE_ADJU && kSub > 0 && usub > 0; };
   // ADJU: the pool chunks this path holds and its ring size, in one word --
   // bits 6j..6j+5: the id of its chunk j (63: none), 24-29: the ring size
   // (a.rec_cap unless the pool ran dry) -- and the wave's free chunks
@@ -1138,7 +1161,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       }
     }
     // ---- refill finished lanes from the wave's range (ballot + mbcnt)
-    const uint64_t need = __ballot(!active);
+    const bool wants = !active && !pending();
+    const uint64_t need = __ballot(wants);
 #ifdef IPT_PHASE_TIMING
     const uint64_t act0_ = ~need;
 #endif
@@ -1169,7 +1193,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     } else if (need) {
       const uint32_t rank =
           __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-      if (!active) {
+      if (wants) {
         const uint64_t w = next + rank;
         if (w < end) {
           set_item(w);
@@ -1184,7 +1208,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           if (MODE == MODE_ADJU) {
             rhi = 0;
             rslot = 0;
-            Mlo = mk(1.f, 1.f, 1.f);
+            if (!kSub) Mlo = mk(1.f, 1.f, 1.f);
             ctab = kNoChunks | ((uint32_t)vmax << 24);
           }
           if (MODE == MODE_GRAPH) {
@@ -1201,7 +1225,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     PHASE(0)
     PHASE_LANES(10, active && !((act0_ >> (tid & 63)) & 1ull))
     // (MODE_FWDM: the last finished slots are summed at the loop top first)
-    if (__ballot(active) == 0 && (MODE != MODE_FWDM || (exhausted && sdone == 0 && fj >= gnp * (uint32_t)a.spp)))
+    if (__ballot(active || pending()) == 0 &&
+        (MODE != MODE_FWDM || (exhausted && sdone == 0 && fj >= gnp * (uint32_t)a.spp)))
       break;
 #ifdef IPT_PHASE_TIMING
     tacc[6] += 1;
@@ -1458,7 +1483,16 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         }
         // a chunk starts at ring slot 0 (vertex j * ring size): the forward's M
         // before the update of its first vertex is the chunk's Mlo
-        if (rslot == 0) Mlo = M;
+        if (kSub > 0) {  // (vertex 0's M is 1: not stored)
+          if (rslot % kSub == 0 && k > 0) {
+            gbl_f32 *m = umr + (size_t)(rslot / kSub) * 192;
+            m[0] = M.x;
+            m[1] = M.y;
+            m[2] = M.z;
+          }
+        } else if (rslot == 0) {
+          Mlo = M;
+        }
         rslot = (rslot + 1 == vcap_of()) ? 0 : rslot + 1;
       }
       if (MODE == MODE_GRAPH) {
@@ -1493,6 +1527,12 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     // terms apply, uesc = the path escaped); urep = replay target (0: none)
     int uhi = 0, ulo = 0, urep = 0;
     bool uend = false, uesc = false;
+    const bool upend = pending();  // a lane with sub-chunks of its chunk left (IPT_ADJU_SUB)
+    if (upend) {  // the chunk of its last sweep: k, rslot, rhi and ctab are untouched since
+      uhi = usub;
+      ulo = rhi == 0 ? k - (rslot == 0 ? vcap_of() : rslot) : rhi - vcap_of();
+      if (ulo > 0) urep = ulo;
+    }
     if (finished) {
       active = false;
       if (MODE == MODE_FWDM) {  // slot [channel][sample]
@@ -1525,6 +1565,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
         if (ulo > 0) urep = ulo;
       }
     }
+    // IPT_ADJU_SUB: this iteration sweeps the chunk's last unswept sub-chunk
+    // [uslo, uhi) (sub-chunks aligned to the chunk's start)
+    const int uslo = (MODE == MODE_ADJU && kSub > 0 && uhi > ulo) ? ulo + kSub * ((uhi - 1 - ulo) / kSub) : ulo;
     if (MODE == MODE_FWDM && __ballot(finished)) {
       // fused pixel mean: each finished lane counts its sample off its slot's
       // table entry (LDS atomic, after the wave's sample writes: a wave's LDS
@@ -1560,7 +1603,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
       // from the chunk's captured Mlo, the last task's suffix is the chunk
       // after's (Scar) unless the chunk ends the path, and the suffix at ulo
       // goes back to the owner for its replay.
-      const int Kf = is_badj<MODE>() ? ((finished && k > 0) ? k : 0) : (uhi > 0 ? uhi - ulo : 0);
+      const int Kf = is_badj<MODE>() ? ((finished && k > 0) ? k : 0) : (uhi > 0 ? uhi - uslo : 0);
       if (__ballot(Kf > 0)) {
         const int lane = tid & 63;
         const int inc = wave_scan_add(Kf);  // inclusive scan of the task counts over the wave
@@ -1599,9 +1642,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           const int st0 = inc - Kf - base;
           const bool owns = Kf > 0 && inc <= next && st0 >= 0;
           const bool oend = is_badj<MODE>() || uend, oesc = is_badj<MODE>() ? escaped : uesc;
+          // (ADJU: the sub-chunk's first ring slot, uslo - ulo, in bits 15-20)
           if (owns)
-            swl[st0] = (((uint32_t)st0 << 15) | (oend ? 1u << 14 : 0u) | (oesc ? 1u << 13 : 0u) |
-                        ((uint32_t)Kf << 6) | (uint32_t)lane) + 1u;
+            swl[st0] = (((uint32_t)st0 << 21) | ((uint32_t)(MODE == MODE_ADJU ? uslo - ulo : 0) << 15) |
+                        (oend ? 1u << 14 : 0u) | (oesc ? 1u << 13 : 0u) | ((uint32_t)Kf << 6) | (uint32_t)lane) + 1u;
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
           const uint32_t mk_ = wave_scan_max(swl[lane]) - 1u;
@@ -1609,7 +1653,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           __builtin_amdgcn_wave_barrier();
           const int ow = valid ? (int)(mk_ & 63u) : lane;
           const int KL = valid ? (int)((mk_ >> 6) & 127u) : 0;
-          const int kk = valid ? lane - (int)(mk_ >> 15) : 0;  // task index inside the path's chunk
+          const int kk = valid ? lane - (int)(mk_ >> 21) : 0;  // task index inside the path's (sub-)chunk
           const bool esc = valid && ((mk_ >> 13) & 1u);
           const bool fst_o = is_badj<MODE>() || (valid && ((mk_ >> 14) & 1u));  // the chunk ends the path
           const int rr = valid ? KL - 1 - kk : 0;  // vertices after this one
@@ -1632,7 +1676,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
               si = r[(kRecSD + 1) * fs];
             }
           } else {
-            const int sl = kk, nl = a.rec_lds;  // the vertex's ring slot (chunks start at slot 0)
+            // the vertex's ring slot (chunks start at slot 0; a sub-chunk at uslo - ulo)
+            const int sl = kk + (valid ? (int)((mk_ >> 15) & 63u) : 0), nl = a.rec_lds;
             constexpr int NF = SPEC ? kRecFieldsSpec : kRecFieldsDiffuse;
             float rv[NF];
             uint32_t cto = 0;  // the owner's pool chunks (uniform branch: its ds_bpermute sees every lane)
@@ -1658,7 +1703,18 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             }
             // (wave-uniform skips: a chunk from vertex 0 has Mlo = 1, and only
             // replay chunks, which paths longer than the ring make, read Scar)
-            if (__ballot(owns && ulo > 0)) Mk = mk(__shfl(Mlo.x, ow), __shfl(Mlo.y, ow), __shfl(Mlo.z, ow));
+            if (kSub > 0) {  // the sub-chunk's first M: captured by the forward (1 at vertex 0)
+              if (__ballot(owns && uslo > 0)) {
+                V3 m0 = mk(1.f, 1.f, 1.f);
+                if (owns && uslo > 0) {
+                  const gbl_f32 *m = umr + (size_t)((uslo - ulo) / kSub) * 192;
+                  m0 = mk(m[0], m[1], m[2]);
+                }
+                Mk = mk(__shfl(m0.x, ow), __shfl(m0.y, ow), __shfl(m0.z, ow));
+              }
+            } else if (__ballot(owns && ulo > 0)) {
+              Mk = mk(__shfl(Mlo.x, ow), __shfl(Mlo.y, ow), __shfl(Mlo.z, ow));
+            }
             if (__ballot(owns && !uend)) Sc = mk(__shfl(Scar.x, ow), __shfl(Scar.y, ow), __shfl(Scar.z, ow));
           }
           // (the min()s keep a mis-indexed record from reaching global memory out of bounds)
@@ -1767,7 +1823,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
             double *grad = karg<double *>(offsetof(TraceKernArgs, grad)) + (a.nscenes > 1 ? (size_t)set * 3 * a.nT : 0);
             bins_add(sl >= 0, grad, sl >= 0 ? (size_t)sl * 3 : (size_t)tk * 3, 3, v);
           }
-          if (MODE == MODE_ADJU && __ballot(owns && urep > 0)) {  // the suffix at the chunk's first vertex, S_lo = A + B S, back to its owner (for its replay)
+          if (MODE == MODE_ADJU && __ballot(owns && (urep > 0 || uslo > ulo))) {  // the suffix at the chunk's first vertex, S_lo = A + B S, back to its owner (for its replay)
             const V3 H = mk(A.x + B.x * S.x, A.y + B.y * S.y, A.z + B.z * S.z);
             const int sa = (owns ? st0 : lane) << 2;
             const V3 Hs = mk(bperm_f(sa, H.x), bperm_f(sa, H.y), bperm_f(sa, H.z));
@@ -1776,8 +1832,12 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           base = next;
         }
       }
+      // IPT_ADJU_SUB: a lane whose chunk has sub-chunks left sweeps the next
+      // one in the next iteration (neither traced nor refilled meanwhile)
+      const bool umore = MODE == MODE_ADJU && kSub > 0 && (finished || upend) && uslo > ulo;
+      if (MODE == MODE_ADJU && kSub > 0) usub = umore ? uslo : 0;
       if (MODE == MODE_ADJU) {  // a path swept to its first vertex gives its pool chunks back
-        const bool rel = finished && urep == 0 && (ctab & kNoChunks) != kNoChunks;
+        const bool rel = (finished || upend) && !umore && urep == 0 && (ctab & kNoChunks) != kNoChunks;
         uint64_t rm = __ballot(rel);
         if (rm) {
           uint64_t mine = 0;
@@ -1795,7 +1855,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           if (rel) ctab |= kNoChunks;
         }
       }
-      if (MODE == MODE_ADJU && urep > 0) {  // replay the path from its camera ray (see the chunk choice)
+      if (MODE == MODE_ADJU && urep > 0 && !umore) {  // replay the path from its camera ray (see the chunk choice)
         int r, c;
         item_ray(a, seed, witem(), st, p, d, r, c);
         L = mk(0.f, 0.f, 0.f);
@@ -2246,6 +2306,7 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.grec = nullptr;
   a.grec_stride = 0;
   a.pool_chunks = 0;
+  a.mring = nullptr;
   a.chunk = 0;
   a.group = 0;
   a.chunk_small = 0;
@@ -2502,7 +2563,7 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
     const int words = std::max(a.nscenes, R);
     if (stream_counters(s, st, words, &b.chunk_ctr, &cap_ctr.p)) return -1;
   }
-  StreamScratch grec;  // ADJU: the vertex-record ring (TraceArgs::grec), freed behind the launch
+  StreamScratch grec, mring;  // ADJU: the vertex-record ring (TraceArgs::grec), freed behind the launch
   if (MODE == MODE_ADJU) {  // the ring's global slots: one chunk pool per wave
     const size_t fields = SPEC ? kRecFieldsSpec : kRecFieldsDiffuse;
     const size_t waves = (size_t)grid * (kBlock / 64), chunk = (size_t)kPoolSlots * fields * sizeof(float);
@@ -2512,6 +2573,10 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
     b.rec_cap = std::min(kAdjuRing, a.rec_lds + kPoolMaxChunks * kPoolSlots);
     if (grec.alloc(waves * b.grec_stride * sizeof(float), st)) return -1;
     b.grec = (float *)grec.p;
+    if (kSub > 0) {  // the captured prefix throughputs of the sub-chunked sweep
+      if (mring.alloc(waves * (size_t)kMrEnt * 64 * 3 * sizeof(float), st)) return -1;
+      b.mring = (float *)mring.p;
+    }
   }
   // (tests: a launch that fails after its counters and scratch are allocated)
   if (g_fail_launches.load() > 0 && g_fail_launches.fetch_sub(1) > 0) {

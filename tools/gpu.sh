@@ -35,6 +35,7 @@
 #   adjpmc       tools/adj_pmc.py: kernel stats + FETCH/WRITE/TCC/TCP passes of the C2 fused render and adjoint,
 #                for the default library, $ADJ_VARIANT (a lib/variants build) and the 5-wave adjoint (IPT_ADJW=0)
 #   counters     rocprofv3 -L (the counters this box offers)
+#   vtests       pytest -m gpu ($VTESTS, -k "$VT_K") against lib/variants/libipt_$VT_VARIANT.so (IPT_AMD_LIB)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 R=$(pwd)
@@ -119,6 +120,9 @@ run() {
                 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/adjstats_var_$T" -o run --output-format csv \
                     -- python3 "$R/tools/adj_pmc.py" --steps 10 > "$OUT/adjstats_var_$T.log" 2>&1 )
             fi ;;
+    vtests) IPT_AMD_LIB=$R/inverse_path_tracer_amd/lib/variants/libipt_$VT_VARIANT.so timeout -k 10 600 \
+                python -u -m pytest ${VTESTS:-tests} -m gpu -v --maxfail=5 --timeout 300 --timeout-method thread \
+                -p no:cacheprovider ${VT_K:+-k "$VT_K"} > "$OUT/pytest_gpu_${VT_VARIANT}_$T.log" 2>&1 ;;
     counters) timeout -k 10 120 rocprofv3 -L > "$OUT/counters_$T.txt" 2>&1 ;;
     pipeab) timeout -k 10 300 python tools/pipeline_ab.py > "$OUT/pipeab_$T.log" 2>&1 ;;
     *) echo "unknown stage $1" >&2; return 2 ;;
