@@ -191,6 +191,13 @@ def cpu_baseline(seconds_per_leg=1.5):
                             "threads": threads}
         L.oro_set_threads(cores)
     c2 = out["c2_fwd_fast_all"]
+    quota = None  # the job's cgroup CPU quota (cpu.max "max_us period_us"), in CPUs
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
     ac = {}
     if "c2_fwd_fast_allcores" in out:
         ac = {"value_allcores": out["c2_fwd_fast_allcores"]["Msamples_s"],
@@ -206,8 +213,10 @@ def cpu_baseline(seconds_per_leg=1.5):
             "graph_value": out["graph_fast_all"]["Msamples_s"],
             "cores_note": "%d = this job's CPU share (OMP_NUM_THREADS on the GPU box; %d CPUs in the affinity mask, "
                           "%d in the machine); value_allcores / grad_value_allcores: the same fast-build C2 forward "
-                          "and C3 adjoint legs on all %d CPUs of the affinity mask"
-                          % (cores, affinity, os.cpu_count() or 0, allc),
+                          "and C3 adjoint legs on all %d CPUs of the affinity mask (cgroup CPU quota: %s CPUs -- "
+                          "threads beyond it time-share the quota)"
+                          % (cores, affinity, os.cpu_count() or 0, allc, "none" if quota is None else quota),
+            "cgroup_cpu_quota": quota,
             "legs": out}
 
 

@@ -184,3 +184,70 @@ def test_wave_pool_hands_out_each_chunk_once(chunks, nl):
         assert dry > 0  # a small pool runs dry: those paths take the shorter ring
     else:
         assert peak < chunks  # q = 0.8 (longer than the scenes' paths): 63 chunks never run out
+
+
+# ---------------------------------------------------------------------------
+# The sub-chunked sweep (ipt_hip.hip, IPT_ADJU_SUB = G): each chunk is swept G
+# vertices at a time from its end, one sub-chunk per loop iteration, the lane
+# idle meanwhile (its k, rslot, rhi and ring size untouched, so the chunk's
+# bounds are recomputed as at its finish); the first M of a sub-chunk comes
+# from the per-lane array the pass fills at every ring slot that is a multiple
+# of G (k > 0; vertex 0's M is 1).
+
+def lane_sweeps_sub(K, nl, grant, G):
+    """Per sweep: (slo, uhi, end, ring slots of [slo, uhi), M capture of
+    slo or 'one', iteration).  Follows the kernel's state machine."""
+    R = min(RING, nl + POOL_MAX * POOL_SLOTS)
+    nch, rhi, it = 0, 0, 0
+    mring = {}
+    while True:
+        rslot, ring, k = 0, {}, 0
+        while True:  # one pass
+            gs = rslot - nl
+            if gs >= 0 and gs % POOL_SLOTS == 0 and gs // POOL_SLOTS >= nch:
+                if grant(nch):
+                    nch += 1
+                else:
+                    R, rslot = rslot, 0
+            if rslot % G == 0 and k > 0:
+                mring[rslot // G] = k  # M before vertex k's update
+            ring[rslot] = k
+            rslot = 0 if rslot + 1 == R else rslot + 1
+            k += 1
+            it += 1
+            if k == K or (rhi > 0 and k == rhi):
+                break
+        usub, first = 0, True
+        while True:  # the finish, then one sub-chunk per iteration
+            uhi = usub if usub else (k if rhi == 0 else rhi)
+            ulo = (k - (R if rslot == 0 else rslot)) if rhi == 0 else rhi - R
+            slo = ulo + G * ((uhi - 1 - ulo) // G)
+            m = "one" if slo == 0 else mring.get((slo - ulo) // G)
+            yield slo, uhi, first and rhi == 0, [ring.get(slo - ulo + i) for i in range(uhi - slo)], m, it
+            first = False
+            if slo > ulo:
+                usub = slo
+                it += 1  # the next sub-chunk in the next iteration
+                continue
+            break
+        if ulo <= 0:
+            return
+        rhi = ulo
+
+
+@pytest.mark.parametrize("G", [4, 8, 16])
+@pytest.mark.parametrize("nl", [1, 6, 8])
+@pytest.mark.parametrize("fail", [0, 2, None])
+@pytest.mark.parametrize("K", list(range(1, 40)) + list(range(40, 80, 3)) + [130, 200])
+def test_sub_chunked_sweep_tiles_the_path(K, nl, fail, G):
+    sweeps = list(lane_sweeps_sub(K, nl, lambda j: fail is None or j < fail, G))
+    cover = []
+    for i, (slo, uhi, end, ring, m, _) in enumerate(sweeps):
+        assert end == (i == 0)                     # only the path's last sub-chunk carries the escape terms
+        assert 0 < uhi - slo <= G                  # a round's chain: at most G - 1 steps
+        assert ring == list(range(slo, uhi))       # task kk reads ring slot slo - ulo + kk
+        assert m == ("one" if slo == 0 else slo)   # the sub-chunk's first M: the pass's capture at slo
+        cover.extend(range(uhi - 1, slo - 1, -1))
+    assert cover == list(range(K - 1, -1, -1))     # every vertex once, last to first
+    its = [s[-1] for s in sweeps]
+    assert its == sorted(its)
