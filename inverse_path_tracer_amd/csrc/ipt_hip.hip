@@ -238,9 +238,10 @@ constexpr int kBvhMinTris = IPT_BVH_MIN_TRIS;
 #endif
 constexpr int kBvhLdsNodeBytes = IPT_BVH_LDS_KB * 1024;  // stage the whole tree in LDS up to 512 nodes
 
-// XCD regions (TraceArgs::nreg, region_count): off in the shipped library
-#ifndef IPT_REGIONS
-#define IPT_REGIONS 1
+// XCD bands (TraceArgs::nband, band_count): the work items of the
+// integrators that read a per-pixel input image, split into IPT_BANDS bands
+#ifndef IPT_BANDS
+#define IPT_BANDS 1
 #endif
 struct TraceArgs {
   int W, H, spp, max_bounces;
@@ -328,7 +329,7 @@ struct TraceArgs {
   // launch on a stream thus starts from zeroed counters in stream order -- no
   // host-side copy of device state, no memset launch per launch, no extra
   // atomic (a count of finished waves cost 2% on the adjoints)
-  uint32_t *chunk_ctr;
+  uint32_t *chunk_ctr;  // word j at chunk_ctr[j * kCtrStride]
   uint32_t grabs;
   // small scenes: acceptance boxes of the pairs (culled shadow casts)
   const PairBox2 *pboxes;
@@ -351,37 +352,23 @@ struct TraceArgs {
   uint32_t mean_off, mean_wstride;
   int nslots;
   uint8_t *ldr;
-  // XCD regions (ADJ, ADJU, GRAPH; one material set): the launch's rows are
-  // split into nreg interleaved sets (launch row lr -> region lr % nreg) and
-  // block b traces region b % nreg only -- the dispatcher deals blocks
-  // round-robin over the 8 XCDs, so a region's pixels (adjoint image, target
-  // image) are read into ONE XCD's L2 instead of all eight (placement only
-  // changes speed, never a result).  Region r is the launch with row0 =
-  // reg_row0[r], row_step * nreg, reg_npix[r] pixels (Lemire constant
-  // reg_m_npix[r]), its own chunk counter (chunk_ctr[r]) and reg_nb[r] big
-  // chunks (guided instances).
-  int nreg;
-  int reg_row0[8];
-  uint32_t reg_nb[8], reg_grabs[8];
-  uint64_t reg_npix[8], reg_m_npix[8];
+  // XCD bands (ADJ, ADJU, GRAPH; one material set, sample-major, 32-bit
+  // indices): the launch's pixels are cut into nband equal contiguous bands
+  // of bnpix pixels, and its work items enumerated band by band -- w = b *
+  // band_items + sj * bnpix + (lp - b * bnpix), sample-major inside a band
+  // (item_split).  Band b has its own chunk counter (chunk_ctr[b]); a block
+  // starts on band blockIdx % nband -- the dispatcher deals blocks
+  // round-robin over the 8 XCDs, so while every band has work left a band's
+  // pixels (adjoint image, target image) are read into ONE XCD's L2 instead
+  // of all eight -- and a wave whose band has run dry takes chunks of the
+  // next bands (the work stays balanced to the end).  Placement only changes
+  // who traces a sample, never its value.  Each band has band_items items,
+  // chunk_big_n big chunks and `grabs` grabs (launch_inst).
+  int nband;
+  uint32_t bnpix;
+  uint64_t band_items, m_band, m_bnpix;
 };
 static_assert(alignof(TraceArgs) == 8, "TraceArgs sits right after the ten 8-B scene pointers in the kernarg segment");
-
-// TraceArgs as region `reg` sees it (TraceArgs::nreg); the per-region
-// fields are read through `src`, the kernarg segment's copy (scalar loads with
-// a wave-uniform offset -- indexing a register copy of the arrays miscompiles)
-template <class SRC>
-__device__ __forceinline__ void region_view(TraceArgs &v, const SRC *src, int reg) {
-  if (IPT_REGIONS > 1 && v.nreg > 1) {  // (regions are compiled in by variant builds only)
-    v.row0 = src->reg_row0[reg];
-    v.row_step *= v.nreg;
-    v.npix = src->reg_npix[reg];
-    v.n_samples = v.npix * (uint64_t)v.spp;
-    v.m_npix = src->reg_m_npix[reg];
-    v.chunk_big_n = src->reg_nb[reg];
-    v.grabs = src->reg_grabs[reg];
-  }
-}
 
 __device__ __forceinline__ uint32_t udiv32(uint32_t n, uint64_t m, uint32_t d) {
   return d == 1u ? n : (uint32_t)__umul64hi(m, (uint64_t)n);
@@ -393,7 +380,13 @@ __device__ __forceinline__ uint32_t udiv32(uint32_t n, uint64_t m, uint32_t d) {
 // [s][pixel][3] buffer -- one contiguous store run).
 __device__ __forceinline__ void item_split(const TraceArgs &a, uint64_t w, uint64_t &lp, uint64_t &sj) {
   if (a.idx32) {
-    if (a.sample_major) {
+    if (IPT_BANDS > 1 && a.nband > 1) {  // banded sample-major (TraceArgs::nband)
+      const uint32_t b = udiv32((uint32_t)w, a.m_band, (uint32_t)a.band_items);
+      const uint32_t wb = (uint32_t)w - b * (uint32_t)a.band_items;
+      const uint32_t q = udiv32(wb, a.m_bnpix, a.bnpix);
+      sj = q;
+      lp = b * a.bnpix + (wb - q * a.bnpix);
+    } else if (a.sample_major) {
       const uint32_t q = udiv32((uint32_t)w, a.m_npix, (uint32_t)a.npix);
       sj = q;
       lp = (uint32_t)w - q * (uint32_t)a.npix;
@@ -424,6 +417,33 @@ __device__ __forceinline__ void local_rc(const TraceArgs &a, uint64_t lp, int &r
   r = a.row0 + (int)lr * a.row_step;
 }
 
+// Guided chunk sizes for the brute-force instances too (IPT_BF_BIG = the big
+// chunks' size in small ones, > 1; see launch_inst): every grab is a
+// device-scope atomic, performed at the memory side (the XCDs' L2s are not
+// coherent), and the launch's grabs queue there -- C2 adjoint 131 072 -> 77 824
+// grabs, 1.816 -> 1.764 ms, the sample-buffer forward 1.629 -> 1.525, scenes/0
+// adjoint 2.276 -> 2.243; 3 or 4 (fewer grabs still) lose some of it, and the
+// fused render's 256-sample grabs are neutral (profiles/r06/variants_bf_r06c.log,
+// variants_ctr_stride_r06e.log)
+#ifndef IPT_BF_BIG
+#define IPT_BF_BIG 2
+#endif
+#ifndef IPT_BF_TAIL
+#define IPT_BF_TAIL 4
+#endif
+// The grab counters' spacing in words: the device-scope atomics on one line
+// are serialised at the memory side, so each word (material set, XCD band)
+// gets a 128-B line of its own.  Eight band words on one line doubled a C2
+// 1/8 share's adjoint (0.31 -> 0.70 ms); one line each: 0.32
+// (profiles/r06/variants_bands_r06d.log, variants_ctr_stride_r06e.log)
+#ifndef IPT_CTR_STRIDE
+#define IPT_CTR_STRIDE 32
+#endif
+constexpr int kCtrStride = IPT_CTR_STRIDE;
+template <bool BVH>
+constexpr bool kGuided() {
+  return BVH || IPT_BF_BIG > 1;
+}
 // Chunk g of a launch (TraceArgs::chunk_big_n) -> units [start, end).
 // GUIDED: the BVH instances (guided_tail); the others take `chunk` units.
 template <bool GUIDED>
@@ -911,20 +931,15 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     umr = (gbl_f32 *)a.mring + ((size_t)blockIdx.x * (kBlock / 64) + (tid >> 6)) * (kMrEnt * 64 * 3) + (tid & 63) * 3;
   {  // the wave's persistent loop
   // wave-uniform sample range (static partition, regenerated per lane)
-  // XCD region (TraceArgs::nreg) of this block, and the wave's index among
-  // the region's waves
-  const int nreg = a.nreg > 1 ? a.nreg : 1;
-  const int reg = nreg > 1 ? (int)(sblock & (uint32_t)(nreg - 1)) : 0;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(((sblock / (uint32_t)nreg) * kBlock + tid) >> 6);
-  const uint32_t nwaves = ((sgrid / (uint32_t)nreg) * kBlock) >> 6;
-  TraceArgs ar = a;
-#if defined(__HIP_DEVICE_COMPILE__)
-  {
-    typedef __attribute__((address_space(4))) const TraceArgs cst_args0;
-    const cst_args0 *k0 = (const cst_args0 *)__builtin_amdgcn_kernarg_segment_ptr();  // TraceArgs is at offset 0
-    region_view(ar, k0, reg);
-  }
-#endif
+  // XCD band (TraceArgs::nband): this block's first band, the wave's index
+  // among the waves that start on it; `band` = the band it takes chunks of
+  // now, `tried` = the bands it has found dry
+  const int nband = IPT_BANDS > 1 && a.nband > 1 ? a.nband : 1;
+  int band = nband > 1 ? (int)(sblock & (uint32_t)(nband - 1)) : 0, tried = 0;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(((sblock / (uint32_t)nband) * kBlock + tid) >> 6);
+  const uint32_t nwaves = ((sgrid / (uint32_t)nband) * kBlock) >> 6;
+  const uint64_t units = nband > 1 ? a.band_items : a.n_samples;  // items per counter
+  const TraceArgs &ar = a;
   // Work items w in [0, n_samples) of this launch (item_split): pixel-major
   // w = lp * spp + s, or sample-major w = s * npix + lp over the launch's
   // pixels lp.  Either way the sample's seed is seed + its global index g:
@@ -936,7 +951,9 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   const bool dyn = a.chunk != 0;
   uint64_t next, end;
   if (dyn) {
-    chunk_range<BVH>(ar, wave, ar.n_samples, next, end);
+    chunk_range<kGuided<BVH>()>(ar, wave, units, next, end);
+    next += (uint64_t)band * units;
+    end += (uint64_t)band * units;
   } else {
     next = (ar.n_samples * wave) / nwaves;
     end = (ar.n_samples * (wave + 1)) / nwaves;
@@ -1087,7 +1104,6 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     const cst_args *apc = (const cst_args *)__builtin_amdgcn_kernarg_segment_ptr();  // first parameter: offset 0
     asm volatile("" : "+s"(apc));
     TraceArgs a = *apc;
-    region_view(a, apc, reg);
 #else
     TraceArgs a = ar;
 #endif
@@ -1110,15 +1126,15 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           bool own = false;
           if (!started) {
             started = true;
-            chunk_range<BVH>(a, wave, a.npix, pl0, pl1);
+            chunk_range<kGuided<BVH>()>(a, wave, a.npix, pl0, pl1);
             own = pl0 < a.npix;
           }
           if (!own) {
             uint32_t c = 0;
-            if (lane == 0) c = atomicAdd(a.chunk_ctr + set, 1u);
+            if (lane == 0) c = atomicAdd(a.chunk_ctr + (size_t)set * kCtrStride, 1u);
             c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);  // lane 0 (full exec here)
-            chunk_range<BVH>(a, nwaves + c, a.npix, pl0, pl1);
-            if (pl0 >= a.npix && lane == 0) grab_failed(a.chunk_ctr + set, c, a.grabs);
+            chunk_range<kGuided<BVH>()>(a, nwaves + c, a.npix, pl0, pl1);
+            if (pl0 >= a.npix && lane == 0) grab_failed(a.chunk_ctr + (size_t)set * kCtrStride, c, a.grabs);
           }
         }
         if (pl0 < a.npix) {
@@ -1143,21 +1159,27 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           exhausted = true;
         }
       }
-    } else if (next >= end && !exhausted) {  // wave-uniform: the next chunk (full exec here)
-      // One counter, grabbed when needed.  Measured against alternatives
-      // (profiles/r02_variants_chunk_*.log): 8 counters on separate lines
-      // with stealing and a grab prefetched one chunk ahead were both slower.
-      uint32_t c = 0;
-      if (lane == 0) c = atomicAdd(a.chunk_ctr + set + reg, 1u);
-      c = (uint32_t)__shfl((int)c, 0);
-      uint64_t start, stop;
-      chunk_range<BVH>(a, nwaves + c, a.n_samples, start, stop);
-      if (start < a.n_samples) {
-        next = start;
-        end = stop;
-      } else {
-        exhausted = true;
-        if (lane == 0) grab_failed(a.chunk_ctr + set + reg, c, a.grabs);
+    } else {
+      // One counter (per band), grabbed when needed.  Measured against
+      // alternatives (profiles/r02_variants_chunk_*.log): 8 counters on
+      // separate lines with stealing and a grab prefetched one chunk ahead
+      // were both slower.  Bands: a wave moves on to the next band after one
+      // failed grab, and stops after one failed grab on every band -- so each
+      // word sees exactly `grabs` grabs per launch (grab_failed).
+      while (next >= end && !exhausted) {  // wave-uniform: the next chunk (full exec here)
+        uint32_t c = 0;
+        if (lane == 0) c = atomicAdd(a.chunk_ctr + (size_t)(set + band) * kCtrStride, 1u);
+        c = (uint32_t)__shfl((int)c, 0);
+        uint64_t start, stop;
+        chunk_range<kGuided<BVH>()>(a, nwaves + c, units, start, stop);
+        if (start < units) {
+          next = (uint64_t)band * units + start;
+          end = (uint64_t)band * units + stop;
+        } else {
+          if (lane == 0) grab_failed(a.chunk_ctr + (size_t)(set + band) * kCtrStride, c, a.grabs);
+          if (++tried >= nband) exhausted = true;
+          band = band + 1 == nband ? 0 : band + 1;
+        }
       }
     }
     // ---- refill finished lanes from the wave's range (ballot + mbcnt)
@@ -2325,12 +2347,9 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.rc_W = (p.width > 0 && (p.width & (p.width - 1)) == 0) ? 1.0f / (float)p.width : 0.f;
   a.rc_H = (p.height > 0 && (p.height & (p.height - 1)) == 0) ? 1.0f / (float)p.height : 0.f;
   a.fused = 0;
-  a.nreg = 1;
-  for (int r = 0; r < 8; ++r) {
-    a.reg_row0[r] = 0;
-    a.reg_nb[r] = a.reg_grabs[r] = 0;
-    a.reg_npix[r] = a.reg_m_npix[r] = 0;
-  }
+  a.nband = 1;
+  a.bnpix = 0;
+  a.band_items = a.m_band = a.m_bnpix = 0;
   a.mean_off = 0;
   a.mean_wstride = 0;
   a.nslots = 0;
@@ -2449,20 +2468,21 @@ static int stream_counters(GpuScene *s, hipStream_t st, int words, uint32_t **ou
   return 0;
 }
 
-// XCD regions of a launch (TraceArgs::nreg) for the integrators that read a
-// per-pixel input image (adjoint, createGraph), one material set: measured
-// (profiles/r04/envab_regions_r04f.log) they cut the C2 adjoint's fetched
-// bytes 25.9 -> 3.8 MB per launch -- every XCD's L2 no longer pulls the whole
-// adjoint image -- but cost 1.6% time (C2 adjoint 1.911 -> 1.942 ms, the
-// unbounded one 4.01 -> 4.15): a region's waves cannot help the region that
-// ends last.  Off in the shipped library (IPT_REGIONS = 1); `make variant
-// DEFS=-DIPT_REGIONS=8` builds them for A/B timing.
+// XCD bands of a launch (TraceArgs::nband) for the integrators that read a
+// per-pixel input image (adjoint, createGraph), one material set.  Round 4's
+// form -- interleaved row regions, block b confined to region b % 8 -- cut the
+// C2 adjoint's fetched bytes 25.9 -> 3.8 MB per launch (every XCD's L2 no
+// longer pulls the whole adjoint image) but cost 1.6% time, since a region's
+// waves could not help the region that ended last
+// (profiles/r04/envab_regions_r04f.log); the bands' waves move on to the
+// other bands' chunks once their own band is dry.  IPT_BANDS = 1: off.
 template <int MODE>
-static int region_count(const TraceArgs &a, int grid) {
-  if (!(is_badj<MODE>() || MODE == MODE_ADJU || MODE == MODE_GRAPH) || a.nscenes > 1 || a.fused) return 1;
-  int R = IPT_REGIONS;
-  const uint64_t rows = a.W > 0 ? a.npix / (uint64_t)a.W : 0;
-  while (R > 1 && ((uint64_t)R > rows || grid % R != 0 || (R & (R - 1)) != 0)) R >>= 1;
+static int band_count(const TraceArgs &a, int grid) {
+  if (!(is_badj<MODE>() || MODE == MODE_ADJU || MODE == MODE_GRAPH) || a.nscenes > 1 || a.fused || !a.idx32 ||
+      !a.sample_major || !IPT_DYN_CHUNKS)
+    return 1;
+  int R = IPT_BANDS;
+  while (R > 1 && (a.npix % (uint64_t)R != 0 || grid % R != 0 || (R & (R - 1)) != 0)) R >>= 1;
   return R;
 }
 
@@ -2514,7 +2534,7 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
   }
   b.chunk = 0;
   b.chunk_ctr = nullptr;
-  b.nreg = 1;
+  b.nband = 1;
   StreamScratch cap_ctr;  // only for a launch captured into a graph
   if (IPT_DYN_CHUNKS) {
     // ~IPT_DYN_CHUNKS_PER_WAVE chunks per wave, a multiple of 64 items, 64..4096
@@ -2533,34 +2553,34 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
       units = a.npix;
     }
     // guided sizes: the last ~IPT_GUIDED_TAIL small chunks per wave end the launch
-    // (non-guided instances: one size, chunk_small = chunk and no big-chunk count)
-    if (!BVH) small = c;
+    // (non-guided instances: one size, chunk_small = chunk and no big-chunk count;
+    // IPT_BF_BIG > 1: big chunks of IPT_BF_BIG x c, then IPT_BF_TAIL chunks of
+    // c per wave -- fewer grabs for the same tail)
+    if (!BVH) {
+      small = c;
+      c *= IPT_BF_BIG;
+    }
     b.chunk = (uint32_t)c;
     b.chunk_small = (uint32_t)small;
-    // per XCD region (one region = the whole launch): its units and big chunks
-    const int R = region_count<MODE>(a, grid);
-    const uint64_t rw = waves / (uint64_t)R, rows = a.npix / (uint64_t)a.W;
-    for (int r = 0; r < R; ++r) {
-      uint64_t ur = units;
-      if (R > 1) {
-        const uint64_t rr = (rows - (uint64_t)r + (uint64_t)R - 1) / (uint64_t)R, np = rr * (uint64_t)a.W;
-        ur = np * (uint64_t)a.spp;
-        b.reg_row0[r] = a.row0 + r * a.row_step;
-        b.reg_npix[r] = np;
-        b.reg_m_npix[r] = np > 1 ? ~0ull / np + 1 : 0;
-      }
-      const uint64_t tail = BVH ? rw * (uint64_t)IPT_GUIDED_TAIL * small : 0;
-      const uint64_t nb = BVH ? (ur > tail ? (ur - tail) / c : 0) : 0;
-      b.reg_nb[r] = (uint32_t)nb;
-      b.reg_grabs[r] = launch_grabs(BVH, ur, c, small, nb, rw);
-      if (r == 0) {
-        b.chunk_big_n = (uint32_t)nb;
-        b.grabs = b.reg_grabs[0];
-      }
+    // per XCD band (one band = the whole launch): its units, big chunks and
+    // grabs -- chunks 0 .. rw-1 of a band are its starting waves' own, every
+    // wave ends with one failed grab on each band
+    const int R = band_count<MODE>(a, grid);
+    const uint64_t rw = waves / (uint64_t)R, ur = units / (uint64_t)R;
+    if (R > 1) {
+      b.nband = R;
+      b.bnpix = (uint32_t)(a.npix / (uint64_t)R);
+      b.band_items = ur;
+      b.m_band = ~0ull / ur + 1;
+      b.m_bnpix = b.bnpix > 1 ? ~0ull / b.bnpix + 1 : 0;
     }
-    b.nreg = R;
+    constexpr bool guided = kGuided<BVH>();
+    const uint64_t tail = guided ? rw * (uint64_t)(BVH ? IPT_GUIDED_TAIL : IPT_BF_TAIL) * small : 0;
+    const uint64_t nb = guided ? (ur > tail ? (ur - tail) / c : 0) : 0;
+    b.chunk_big_n = (uint32_t)nb;
+    b.grabs = launch_grabs(guided, ur, c, small, nb, rw) + (uint32_t)((R - 1) * rw);
     cap_ctr.st = st;
-    const int words = std::max(a.nscenes, R);
+    const int words = std::max(a.nscenes, R) * kCtrStride;  // (bands: one material set)
     if (stream_counters(s, st, words, &b.chunk_ctr, &cap_ctr.p)) return -1;
   }
   StreamScratch grec, mring;  // ADJU: the vertex-record ring (TraceArgs::grec), freed behind the launch

@@ -6,7 +6,7 @@
 import re
 import sys
 
-MODES = {"0": "FWD", "1": "ADJ", "2": "GRAPH", "3": "ADJU"}
+MODES = {"0": "FWD", "1": "ADJ", "2": "GRAPH", "3": "ADJU", "4": "FWDM", "5": "ADJW"}
 rows, cur = [], None
 for line in open(sys.argv[1], errors="replace"):
     m = re.search(r"Function Name: (\S+)", line)
