@@ -238,11 +238,6 @@ constexpr int kBvhMinTris = IPT_BVH_MIN_TRIS;
 #endif
 constexpr int kBvhLdsNodeBytes = IPT_BVH_LDS_KB * 1024;  // stage the whole tree in LDS up to 512 nodes
 
-// XCD bands (TraceArgs::nband, band_count): the work items of the
-// integrators that read a per-pixel input image, split into IPT_BANDS bands
-#ifndef IPT_BANDS
-#define IPT_BANDS 1
-#endif
 struct TraceArgs {
   int W, H, spp, max_bounces;
   uint64_t seed;
@@ -352,21 +347,6 @@ struct TraceArgs {
   uint32_t mean_off, mean_wstride;
   int nslots;
   uint8_t *ldr;
-  // XCD bands (ADJ, ADJU, GRAPH; one material set, sample-major, 32-bit
-  // indices): the launch's pixels are cut into nband equal contiguous bands
-  // of bnpix pixels, and its work items enumerated band by band -- w = b *
-  // band_items + sj * bnpix + (lp - b * bnpix), sample-major inside a band
-  // (item_split).  Band b has its own chunk counter (chunk_ctr[b]); a block
-  // starts on band blockIdx % nband -- the dispatcher deals blocks
-  // round-robin over the 8 XCDs, so while every band has work left a band's
-  // pixels (adjoint image, target image) are read into ONE XCD's L2 instead
-  // of all eight -- and a wave whose band has run dry takes chunks of the
-  // next bands (the work stays balanced to the end).  Placement only changes
-  // who traces a sample, never its value.  Each band has band_items items,
-  // chunk_big_n big chunks and `grabs` grabs (launch_inst).
-  int nband;
-  uint32_t bnpix;
-  uint64_t band_items, m_band, m_bnpix;
 };
 static_assert(alignof(TraceArgs) == 8, "TraceArgs sits right after the ten 8-B scene pointers in the kernarg segment");
 
@@ -380,13 +360,7 @@ __device__ __forceinline__ uint32_t udiv32(uint32_t n, uint64_t m, uint32_t d) {
 // [s][pixel][3] buffer -- one contiguous store run).
 __device__ __forceinline__ void item_split(const TraceArgs &a, uint64_t w, uint64_t &lp, uint64_t &sj) {
   if (a.idx32) {
-    if (IPT_BANDS > 1 && a.nband > 1) {  // banded sample-major (TraceArgs::nband)
-      const uint32_t b = udiv32((uint32_t)w, a.m_band, (uint32_t)a.band_items);
-      const uint32_t wb = (uint32_t)w - b * (uint32_t)a.band_items;
-      const uint32_t q = udiv32(wb, a.m_bnpix, a.bnpix);
-      sj = q;
-      lp = b * a.bnpix + (wb - q * a.bnpix);
-    } else if (a.sample_major) {
+    if (a.sample_major) {
       const uint32_t q = udiv32((uint32_t)w, a.m_npix, (uint32_t)a.npix);
       sj = q;
       lp = (uint32_t)w - q * (uint32_t)a.npix;
@@ -432,10 +406,12 @@ __device__ __forceinline__ void local_rc(const TraceArgs &a, uint64_t lp, int &r
 #define IPT_BF_TAIL 4
 #endif
 // The grab counters' spacing in words: the device-scope atomics on one line
-// are serialised at the memory side, so each word (material set, XCD band)
-// gets a 128-B line of its own.  Eight band words on one line doubled a C2
-// 1/8 share's adjoint (0.31 -> 0.70 ms); one line each: 0.32
-// (profiles/r06/variants_bands_r06d.log, variants_ctr_stride_r06e.log)
+// are serialised at the memory side, so each word (material set) gets a
+// 128-B line of its own.  Eight words on one line (round 6's XCD bands,
+// DESIGN.md §12.2) doubled a C2 1/8 share's adjoint (0.31 -> 0.70 ms), one
+// line each: 0.32; the C2 adjoint 1.796 -> 1.768 ms with it
+// (profiles/r06/variants_bands_r06d.log, variants_ctr_stride_r06e.log,
+// variants_grab_r06h.log)
 #ifndef IPT_CTR_STRIDE
 #define IPT_CTR_STRIDE 32
 #endif
@@ -931,14 +907,8 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
     umr = (gbl_f32 *)a.mring + ((size_t)blockIdx.x * (kBlock / 64) + (tid >> 6)) * (kMrEnt * 64 * 3) + (tid & 63) * 3;
   {  // the wave's persistent loop
   // wave-uniform sample range (static partition, regenerated per lane)
-  // XCD band (TraceArgs::nband): this block's first band, the wave's index
-  // among the waves that start on it; `band` = the band it takes chunks of
-  // now, `tried` = the bands it has found dry
-  const int nband = IPT_BANDS > 1 && a.nband > 1 ? a.nband : 1;
-  int band = nband > 1 ? (int)(sblock & (uint32_t)(nband - 1)) : 0, tried = 0;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(((sblock / (uint32_t)nband) * kBlock + tid) >> 6);
-  const uint32_t nwaves = ((sgrid / (uint32_t)nband) * kBlock) >> 6;
-  const uint64_t units = nband > 1 ? a.band_items : a.n_samples;  // items per counter
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((sblock * kBlock + tid) >> 6);
+  const uint32_t nwaves = (sgrid * kBlock) >> 6;
   const TraceArgs &ar = a;
   // Work items w in [0, n_samples) of this launch (item_split): pixel-major
   // w = lp * spp + s, or sample-major w = s * npix + lp over the launch's
@@ -951,9 +921,7 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
   const bool dyn = a.chunk != 0;
   uint64_t next, end;
   if (dyn) {
-    chunk_range<kGuided<BVH>()>(ar, wave, units, next, end);
-    next += (uint64_t)band * units;
-    end += (uint64_t)band * units;
+    chunk_range<kGuided<BVH>()>(ar, wave, ar.n_samples, next, end);
   } else {
     next = (ar.n_samples * wave) / nwaves;
     end = (ar.n_samples * (wave + 1)) / nwaves;
@@ -1159,27 +1127,22 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           exhausted = true;
         }
       }
-    } else {
-      // One counter (per band), grabbed when needed.  Measured against
-      // alternatives (profiles/r02_variants_chunk_*.log): 8 counters on
-      // separate lines with stealing and a grab prefetched one chunk ahead
-      // were both slower.  Bands: a wave moves on to the next band after one
-      // failed grab, and stops after one failed grab on every band -- so each
-      // word sees exactly `grabs` grabs per launch (grab_failed).
-      while (next >= end && !exhausted) {  // wave-uniform: the next chunk (full exec here)
-        uint32_t c = 0;
-        if (lane == 0) c = atomicAdd(a.chunk_ctr + (size_t)(set + band) * kCtrStride, 1u);
-        c = (uint32_t)__shfl((int)c, 0);
-        uint64_t start, stop;
-        chunk_range<kGuided<BVH>()>(a, nwaves + c, units, start, stop);
-        if (start < units) {
-          next = (uint64_t)band * units + start;
-          end = (uint64_t)band * units + stop;
-        } else {
-          if (lane == 0) grab_failed(a.chunk_ctr + (size_t)(set + band) * kCtrStride, c, a.grabs);
-          if (++tried >= nband) exhausted = true;
-          band = band + 1 == nband ? 0 : band + 1;
-        }
+    } else if (next >= end && !exhausted) {  // wave-uniform: the next chunk (full exec here)
+      // One counter, grabbed when needed.  Measured against alternatives
+      // (profiles/r02_variants_chunk_*.log): 8 counters on separate lines
+      // with stealing and a grab prefetched one chunk ahead were both slower
+      // (and round 6's XCD bands).
+      uint32_t c = 0;
+      if (lane == 0) c = atomicAdd(a.chunk_ctr + (size_t)set * kCtrStride, 1u);
+      c = (uint32_t)__shfl((int)c, 0);
+      uint64_t start, stop;
+      chunk_range<kGuided<BVH>()>(a, nwaves + c, a.n_samples, start, stop);
+      if (start < a.n_samples) {
+        next = start;
+        end = stop;
+      } else {
+        exhausted = true;
+        if (lane == 0) grab_failed(a.chunk_ctr + (size_t)set * kCtrStride, c, a.grabs);
       }
     }
     // ---- refill finished lanes from the wave's range (ballot + mbcnt)
@@ -2347,9 +2310,6 @@ static TraceArgs make_args(const GpuScene *s, const RenderParams &p) {
   a.rc_W = (p.width > 0 && (p.width & (p.width - 1)) == 0) ? 1.0f / (float)p.width : 0.f;
   a.rc_H = (p.height > 0 && (p.height & (p.height - 1)) == 0) ? 1.0f / (float)p.height : 0.f;
   a.fused = 0;
-  a.nband = 1;
-  a.bnpix = 0;
-  a.band_items = a.m_band = a.m_bnpix = 0;
   a.mean_off = 0;
   a.mean_wstride = 0;
   a.nslots = 0;
@@ -2468,24 +2428,6 @@ static int stream_counters(GpuScene *s, hipStream_t st, int words, uint32_t **ou
   return 0;
 }
 
-// XCD bands of a launch (TraceArgs::nband) for the integrators that read a
-// per-pixel input image (adjoint, createGraph), one material set.  Round 4's
-// form -- interleaved row regions, block b confined to region b % 8 -- cut the
-// C2 adjoint's fetched bytes 25.9 -> 3.8 MB per launch (every XCD's L2 no
-// longer pulls the whole adjoint image) but cost 1.6% time, since a region's
-// waves could not help the region that ended last
-// (profiles/r04/envab_regions_r04f.log); the bands' waves move on to the
-// other bands' chunks once their own band is dry.  IPT_BANDS = 1: off.
-template <int MODE>
-static int band_count(const TraceArgs &a, int grid) {
-  if (!(is_badj<MODE>() || MODE == MODE_ADJU || MODE == MODE_GRAPH) || a.nscenes > 1 || a.fused || !a.idx32 ||
-      !a.sample_major || !IPT_DYN_CHUNKS)
-    return 1;
-  int R = IPT_BANDS;
-  while (R > 1 && (a.npix % (uint64_t)R != 0 || grid % R != 0 || (R & (R - 1)) != 0)) R >>= 1;
-  return R;
-}
-
 // Guided chunk sizes (TraceArgs::chunk_big_n), BVH instances: a launch hands
 // out its last ~IPT_GUIDED_TAIL small chunks per wave (64 work items) after
 // the big ones, so the waves that take the last chunks finish close to the
@@ -2534,7 +2476,6 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
   }
   b.chunk = 0;
   b.chunk_ctr = nullptr;
-  b.nband = 1;
   StreamScratch cap_ctr;  // only for a launch captured into a graph
   if (IPT_DYN_CHUNKS) {
     // ~IPT_DYN_CHUNKS_PER_WAVE chunks per wave, a multiple of 64 items, 64..4096
@@ -2562,25 +2503,14 @@ static int launch_inst(GpuScene *s, const TraceArgs &a, size_t lds, const float 
     }
     b.chunk = (uint32_t)c;
     b.chunk_small = (uint32_t)small;
-    // per XCD band (one band = the whole launch): its units, big chunks and
-    // grabs -- chunks 0 .. rw-1 of a band are its starting waves' own, every
-    // wave ends with one failed grab on each band
-    const int R = band_count<MODE>(a, grid);
-    const uint64_t rw = waves / (uint64_t)R, ur = units / (uint64_t)R;
-    if (R > 1) {
-      b.nband = R;
-      b.bnpix = (uint32_t)(a.npix / (uint64_t)R);
-      b.band_items = ur;
-      b.m_band = ~0ull / ur + 1;
-      b.m_bnpix = b.bnpix > 1 ? ~0ull / b.bnpix + 1 : 0;
-    }
+    const uint64_t rw = waves;  // chunks 0 .. rw-1: the waves' own; every wave ends with one failed grab
     constexpr bool guided = kGuided<BVH>();
     const uint64_t tail = guided ? rw * (uint64_t)(BVH ? IPT_GUIDED_TAIL : IPT_BF_TAIL) * small : 0;
-    const uint64_t nb = guided ? (ur > tail ? (ur - tail) / c : 0) : 0;
+    const uint64_t nb = guided ? (units > tail ? (units - tail) / c : 0) : 0;
     b.chunk_big_n = (uint32_t)nb;
-    b.grabs = launch_grabs(guided, ur, c, small, nb, rw) + (uint32_t)((R - 1) * rw);
+    b.grabs = launch_grabs(guided, units, c, small, nb, rw);
     cap_ctr.st = st;
-    const int words = std::max(a.nscenes, R) * kCtrStride;  // (bands: one material set)
+    const int words = a.nscenes * kCtrStride;
     if (stream_counters(s, st, words, &b.chunk_ctr, &cap_ctr.p)) return -1;
   }
   StreamScratch grec, mring;  // ADJU: the vertex-record ring (TraceArgs::grec), freed behind the launch
