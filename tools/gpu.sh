@@ -11,6 +11,7 @@
 #   bench        bench.py (full JSON line)
 #   benchq       bench.py --no-secondary --no-cpu-baseline
 #   benchd       bench.py exactly as the driver runs it (--gpus 1 --steps 20 --warmup 5)
+#   benchrep     the driver's form three times back to back (run-to-run spread in one box)
 #   benchsteps   headline only (--no-secondary --no-cpu-baseline) at 20 / 60 / 200 steps, warmup 5
 #   prof         rocprofv3 --kernel-trace --stats of the C2 headline (no secondary lines)
 #   pmc          FETCH_SIZE / WRITE_SIZE passes of the C2 headline (separate runs)
@@ -82,6 +83,10 @@ run() {
                   timeout -k 10 300 python3 bench.py --steps $k --warmup 5 --no-secondary --no-cpu-baseline \
                       >> "$OUT/benchsteps_$T.jsonl" 2>> "$OUT/benchsteps_$T.err" || return 1
                 done ;;
+    benchrep) for k in 1 2 3; do
+                timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/benchrep_${T}_$k.json" \
+                    2> "$OUT/benchrep_${T}_$k.err" || return 1
+              done ;;
     benchq) timeout -k 10 300 python bench.py --no-secondary --no-cpu-baseline > "$OUT/benchq_$T.json" 2> "$OUT/benchq_$T.err" ;;
     prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$T" -o run --output-format csv \
               -- python3 "$R/bench.py" --steps 20 --warmup 2 --no-cpu-baseline --no-secondary > "$OUT/prof_$T.log" 2>&1 ;;

@@ -101,13 +101,17 @@ def main():
         pr8 = N.make_params(512, 512, 64, 4, 0, 0, 512, 8)  # one interleaved 1/8 share (the bench's tile split)
         hdr = torch.empty((512 * 512, 3), device=dev)
         pu = N.make_params(512, 512, 64, None, 0)  # the reference's own estimator (no bounce cap)
-        kinds = ("fwd", "fsm", "adj", "band", "render", "render8", "adj8", "adju", "renderu")
+        # adj5: the bounded adjoint with IPT_ADJW=0 (the 5-wave instance; the
+        # library reads the variable at each launch)
+        kinds = ("fwd", "fsm", "adj", "band", "render", "render8", "adj8", "adju", "renderu", "adj5")
         times = {n: {k: [] for k in kinds} for n in libs}
         for rnd in range(6):
             for n, L in libs.items():
                 for kind in kinds:
                     if kind == "fsm" and not hasattr(L, "ipt_render_samples_sm_dev"):
                         continue
+                    if kind == "adj5":
+                        os.environ["IPT_ADJW"] = "0"
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
                     for _ in range(3):
@@ -128,6 +132,7 @@ def main():
                             assert L.ipt_adjoint_dev(hs[n], C.byref(p), None, adj.data_ptr(), g.data_ptr(), st) == 0
                     e1.record()
                     torch.cuda.synchronize()
+                    os.environ.pop("IPT_ADJW", None)
                     if rnd > 0:
                         times[n][kind].append(e0.elapsed_time(e1) / 3)
         for n in libs:
@@ -140,6 +145,7 @@ def main():
                                     "adj8_ms": round(float(np.median(times[n]["adj8"])), 4),
                                     "adju_ms": round(float(np.median(times[n]["adju"])), 4),
                                     "renderu_ms": round(float(np.median(times[n]["renderu"])), 4),
+                                    "adj5_ms": round(float(np.median(times[n]["adj5"])), 4),
                                     "fwd_Msps": round(512 * 512 * 64 / f / 1e3, 1), "adj_Msps": round(512 * 512 * 64 / a / 1e3, 1)}
             print(sname, n, out[sname + ":" + n], flush=True)
     print(json.dumps(out))
