@@ -145,3 +145,81 @@ def test_host_only_scene_refuses_render():
         s.render(8, 8, 1, 2, 0)
     with pytest.raises(NativeError):
         s.adjoint(np.zeros((8, 8, 3), np.float32), 8, 8, 1, 2, 0)
+
+
+def _num(rs):
+    """A decimal in one of the spellings tryParseDouble accepts (utils.h:70-200):
+    signs, leading/trailing dots, e/E exponents with signs, long mantissas."""
+    m = rs.uniform(-3, 3)
+    k = rs.randint(8)
+    if k == 0:
+        return "%d" % int(round(m * 3))
+    if k == 1:
+        return ("%.9f" % m).rstrip("0")
+    if k == 2:
+        return ("+" if m >= 0 else "") + "%.6g" % m
+    if k == 3:
+        s = "%.5f" % abs(m)
+        return ("-" if m < 0 else "") + (s[1:] if s.startswith("0.") else s)  # ".123"
+    if k == 4:
+        return "%.4e" % m
+    if k == 5:
+        return ("%.3E" % (m * 1e-3)).replace("E-0", "E-")
+    if k == 6:
+        return "%.22f" % m  # more digits than a double holds
+    return "%de%+d" % (int(m * 1000), rs.randint(-4, 2))
+
+
+def _random_obj(rs):
+    nv = rs.randint(4, 12)
+    lines = ["# fuzz", "mtllib fuzz.mtl"]
+    for _ in range(nv):
+        lines.append("v %s %s %s" % (_num(rs), _num(rs), _num(rs)))
+    nvn = rs.randint(0, 3)
+    for _ in range(nvn):
+        lines.append("vn %s %s %s" % (_num(rs), _num(rs), _num(rs)))
+    lines.append("vt 0 0")
+    mats = ["a", "b", "nope"]
+    for f in range(rs.randint(1, 6)):
+        if rs.randint(3) == 0:
+            lines.append("usemtl " + mats[rs.randint(3)])
+        n = rs.randint(3, min(7, nv + 1))
+        idx = rs.choice(nv, size=n, replace=False) + 1
+        toks = []
+        use_n = nvn > 0 and rs.randint(2) == 0
+        for i in idx:
+            vi = str(i) if rs.randint(4) else str(i - nv - 1)  # negative (relative) indices
+            if use_n:
+                toks.append("%s//%d" % (vi, rs.randint(nvn) + 1))
+            elif rs.randint(4) == 0:
+                toks.append("%s/1" % vi)
+            else:
+                toks.append(vi)
+        lines.append("f " + " ".join(toks))
+    return "\n".join(lines) + "\n"
+
+
+MTL_FUZZ = """newmtl a
+Kd 0.5 .25 1e-1
+Ke 0 0 0
+newmtl b
+Kd 0.9 0.1 0.3
+Ks 0.2 0.2 0.2
+Ns 7
+"""
+
+
+@pytest.mark.parametrize("seed", range(200))
+def test_fuzzed_obj_files_bitwise(oracle, tmp_path, seed):
+    """Random OBJ texts (number spellings, polygons up to 6 sides, negative
+    indices, v//vn and v/vt faces, material switches) through a random object
+    transform: the product's loader equals the oracle's bit for bit."""
+    rs = np.random.RandomState(1000 + seed)
+    obj = tmp_path / "fuzz.obj"
+    mtl = tmp_path / "fuzz.mtl"
+    obj.write_text(_random_obj(rs))
+    mtl.write_text(MTL_FUZZ)
+    pos = tuple(float(x) for x in rs.uniform(-2, 2, 3))
+    ori = tuple(float(x) for x in rs.uniform(-1.5, 1.5, 3)) if seed % 3 else (0.0, 0.0, 0.0)
+    scl = tuple(float(x) for x in rs.uniform(0.3, 2.5, 3))
+    _same([(pos, ori, scl, str(obj), str(mtl))], oracle)
