@@ -223,3 +223,39 @@ def test_fuzzed_obj_files_bitwise(oracle, tmp_path, seed):
     ori = tuple(float(x) for x in rs.uniform(-1.5, 1.5, 3)) if seed % 3 else (0.0, 0.0, 0.0)
     scl = tuple(float(x) for x in rs.uniform(0.3, 2.5, 3))
     _same([(pos, ori, scl, str(obj), str(mtl))], oracle)
+
+
+def _random_mtl(rs, names):
+    keys = ["Kd", "Ks", "Ke", "Ka", "Tf"]
+    out = ["# fuzzed materials"]
+    for nm in names + [names[rs.randint(len(names))]]:  # one name defined twice
+        out.append(("\t" if rs.randint(3) == 0 else "") + "newmtl " + nm)
+        for _ in range(rs.randint(1, 6)):
+            k = rs.randint(8)
+            ind = " " * rs.randint(3)
+            if k < 5:
+                v = [_num(rs).lstrip("-") for _ in range(3)]  # colours >= 0
+                out.append("%s%s %s" % (ind, keys[k], " ".join(v if rs.randint(4) else v[:1])))
+            elif k == 5:
+                out.append("%sNs %s" % (ind, _num(rs).lstrip("-")))
+            elif k == 6:
+                out.append("%sillum %d" % (ind, rs.randint(3)))
+            else:
+                out.append("%sd %s" % (ind, _num(rs).lstrip("-")))
+        if rs.randint(3) == 0:
+            out.append("")
+    return ("\r\n" if rs.randint(2) else "\n").join(out) + "\n"
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_fuzzed_mtl_files_bitwise(oracle, tmp_path, seed):
+    """Random MTL texts (Kd/Ks/Ke with one or three values, Ns, unknown keys,
+    indentation, CRLF, a material defined twice) under a fixed mesh: the
+    product's materials equal the oracle's bit for bit."""
+    rs = np.random.RandomState(5000 + seed)
+    obj = tmp_path / "m.obj"
+    mtl = tmp_path / "m.mtl"
+    obj.write_text("mtllib m.mtl\nv 0 0 0\nv 1 0 0\nv 1 1 0\nv 0 1 0\nv 0 0 1\n"
+                   "usemtl a\nf 1 2 3\nusemtl b\nf 1 3 4\nusemtl c\nf 1 2 5\nf 2 3 5 4\n")
+    mtl.write_text(_random_mtl(rs, ["a", "b", "c"]))
+    _same([((0, 0, 3), (0, 0, 0), (1, 1, 1), str(obj), str(mtl))], oracle)
