@@ -34,7 +34,8 @@ BUDGET = {
     (2, False, True): 0,
     (1, False, True): 0,    # BVH adjoint (2 waves/SIMD, 256 VGPRs allowed)
     (3, False, True): 0,
-    (3, False, False): 8,   # unbounded adjoint: 1 spilled VGPR (pool chunks, round 5; was 3)
+    (3, False, False): 12,  # unbounded adjoint: pool chunks (round 5: 8 B; round 6: 12 B with the uniform-region
+                            # flag, DESIGN.md §12.9, under which this launch is 1.2-1.4% faster)
     (0, False, True): 0,    # BVH forward: the work item, source triangle and Le in LDS (round 5; was 44-52 B)
     # SPEC instances (materials with a Phong lobe): pow_d out of line keeps its
     # constants out of the trace loop (round 4: 164-292 B per lane)
