@@ -566,12 +566,22 @@ constexpr int min_blocks() {
 #ifndef IPT_GRAPH_LDS_KB
 #define IPT_GRAPH_LDS_KB 64
 #endif
-// Work enumeration of the adjoint and graph integrators: sample-major -- a
-// wave's 64 lanes trace 64 different pixels, so their paths diverge at once:
-// the LDS atomics of a vertex step hit different bins and few lanes of a wave
-// need the BVH tree in the same step (pixel-major: 64 samples of one pixel,
-// whose first vertices land on the same triangle, C2 adjoint 3.29 -> 3.24 ms,
-// sphere 23.8 -> 16.3 ms, profiles/r01_variants_adj_sample_major.log).
+// Work enumeration of the adjoint and graph integrators.  Round 1 chose
+// sample-major (a wave's 64 lanes trace 64 different pixels, so the LDS
+// atomics of a vertex step hit different bins and few lanes need the BVH tree
+// at once: C2 adjoint 3.29 -> 3.24 ms, sphere 23.8 -> 16.3 ms,
+// profiles/r01_variants_adj_sample_major.log).  Since the culled casts and the
+// wave-parallel sweep, pixel-major is the faster adjoint (a wave's coherent
+// rays skip more pair blocks; C2 1.747 -> 1.734 ms, scenes/0 unbounded
+// 3.554 -> 3.502, north star 3.905 -> 3.835, profiles/r06/variants_adj_enumeration_r06t.log)
+// and each pixel's adjoint value is fetched by one chunk, i.e. one XCD's L2
+// (DESIGN.md §12.10).  IPT_ADJ_PIXEL_MAJOR / IPT_GRAPH_PIXEL_MAJOR select it.
+#ifndef IPT_ADJ_PIXEL_MAJOR
+#define IPT_ADJ_PIXEL_MAJOR 1
+#endif
+#ifndef IPT_GRAPH_PIXEL_MAJOR
+#define IPT_GRAPH_PIXEL_MAJOR 1
+#endif
 #define IPT_TRACE_BOUNDS __attribute__((amdgpu_flat_work_group_size(1, kBlock), amdgpu_waves_per_eu(min_blocks<MODE, BVH>() ? min_blocks<MODE, BVH>() : 1)))
 // Profiling-only build (make variant DEFS=-DIPT_PHASE_TIMING): each wave
 // accumulates s_memtime cycles per phase of the loop; read with
@@ -2770,7 +2780,7 @@ int gpu_adjoint(GpuScene *s, const RenderParams &p, const float *kd_dev, const f
     return -1;
   }
   TraceArgs a = make_args(s, p);
-  a.sample_major = 1;  // sample-major (see IPT_TRACE_BOUNDS)
+  a.sample_major = IPT_ADJ_PIXEL_MAJOR ? 0 : 1;  // (see IPT_ADJ_PIXEL_MAJOR)
   if (s->grad_map) {
     a.grad_slots = kLdsGradBytes / (3 * (int)sizeof(double));
     a.grad_map = s->grad_map;
@@ -2847,7 +2857,7 @@ int gpu_graph(GpuScene *s, const RenderParams &p, const uint8_t *target_dev, dou
   const size_t bins = graph_lds_doubles(s->host.nT, s->host.nE) * sizeof(double);
   a.lds_edges = bins <= (size_t)IPT_GRAPH_LDS_KB * 1024 ? 1 : 0;
   a.kd_tables = 0;  // the graph integrator never reads albedo
-  a.sample_major = 1;
+  a.sample_major = IPT_GRAPH_PIXEL_MAJOR ? 0 : 1;  // (see IPT_ADJ_PIXEL_MAJOR)
   return launch<MODE_GRAPH>(s, a, (a.lds_edges ? bins : 0) + table_bytes(a), nullptr, nullptr, nullptr, nullptr, target_dev, acc_dev,
                             (hipStream_t)stream);
 }
