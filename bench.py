@@ -589,14 +589,17 @@ def main():
     achieved = flop_per_launch / (kernel_ms / 1e3) / 1e12
     # the adjoint kernel over the same casts (its step also holds the gradient memset + all-reduce)
     grad_achieved = flop_per_launch / (bwd_serial_ms / args.steps / 1e3) / 1e12  # the launch's own time
-    traffic = None
+    traffic = grad_traffic = None
     if os.path.exists(PMC_FILE):
         with open(PMC_FILE) as f:
             pmc = json.load(f)
         if "trace_kernel<4" in pmc.get("kernel", ""):  # counters of the kernel timed here (the fused render)
             traffic = pmc.get("hbm_bytes_per_launch")
-        if world > 1 and traffic:
-            traffic = traffic * band_samples / frame  # the counters were taken on the whole frame
+        if "trace_kernel<5" in pmc.get("grad_kernel", ""):  # and of the 6-wave adjoint the gradient leg runs
+            grad_traffic = pmc.get("grad_hbm_bytes_per_launch")
+        if world > 1:  # the counters were taken on the whole frame
+            traffic = traffic * band_samples / frame if traffic else traffic
+            grad_traffic = grad_traffic * band_samples / frame if grad_traffic else grad_traffic
     hbm = None
     if traffic:
         gbs = traffic / (kernel_ms / 1e3) / 1e9
@@ -604,8 +607,12 @@ def main():
                "frac": round(gbs / 8000.0, 4), "algorithmic_bytes_per_launch": head.npix * 12,
                "algorithmic": "the 12 B/pixel HDR output (compulsory)",
                "source": os.path.relpath(PMC_FILE, ROOT)}
+        if grad_traffic:
+            hbm["grad_bytes_per_launch"] = grad_traffic
+            hbm["grad_achieved_GBps"] = round(grad_traffic / (bwd_serial_ms / args.steps / 1e3) / 1e9, 1)
+            hbm["grad_algorithmic"] = "the 12 B/pixel adjoint image read once (%d B)" % (head.npix * 12)
     roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
+                "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic, "grad_traffic": grad_traffic,
                 # SURVEY.md 8(d) fixes `frac`'s formula (brute-force-equivalent tests, judge and builder
                 # alike); the same number under its descriptive name, and `executed_frac` below
                 "brute_force_equivalent_frac": round(achieved / PEAK_FP32_TFLOPS, 4),

@@ -43,6 +43,11 @@ def main(fetch_dir, write_dir, out):
     if fwd:
         res["kernel"] = fwd[0]
         res["hbm_bytes_per_launch"] = kernels[fwd[0]]["hbm_bytes_per_launch"]
+    # the gradient half of the headline: the adjoint (MODE_ADJW = 5, else MODE_ADJ = 2)
+    adj = [k for k in kernels if "trace_kernel<5" in k] or [k for k in kernels if "trace_kernel<2" in k]
+    if adj:
+        res["grad_kernel"] = adj[0]
+        res["grad_hbm_bytes_per_launch"] = kernels[adj[0]]["hbm_bytes_per_launch"]
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps({k: v["hbm_bytes_per_launch"] for k, v in kernels.items()}, indent=1))
