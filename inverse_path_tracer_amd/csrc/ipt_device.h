@@ -92,73 +92,35 @@ __device__ __forceinline__ float uniform(Rng &s) {
   return (float)(s.v4 + s.d) * 2.3283064e-10f + 1.1641532e-10f;
 }
 
+// ------------------------------------------------------------ sin/cos(phi)
+// sinf/cosf of the float angle phi in [0, 2pi] (path_trace.cu:92,96: `phi` is
+// a float, so the reference's sin(phi)/cos(phi) are CUDA's float sinf/cosf,
+// documented to 2 ulp) in float arithmetic -- rounds 1-6 evaluated them in
+// double (27 FP64 operations per vertex; C2 render -3.6%, adjoint -2.8% with
+// this form): three-part Cody-Waite reduction by
+// pi/2 (the first step exact: k <= 4), Cephes' degree-7 sine and degree-8
+// cosine on |r| <= pi/4.  Every operation is an explicit IEEE fmaf / mul /
+// rint, so oracle/ipt_oracle.c::oro_sincos reproduces it bit for bit;
+// exhaustively over the floats of [1e-10, 6.2832]: at most 1.49 / 1.56 ulp;
+// 76% of uniformly drawn angles correctly rounded (tests/test_oracle.py).
+__device__ __forceinline__ void sincos_f(float x, float &sf, float &cf) {
+  const float k = rintf(x * 0x1.45f306p-1f);  // 2/pi
+  float r = fmaf(-k, 0x1.921fb6p+0f, x);      // pi/2 = C1 + C2 + C3
+  r = fmaf(-k, -0x1.777a5cp-25f, r);
+  r = fmaf(-k, -0x1.ee59dap-50f, r);
+  const float z = r * r;
+  float p = fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f);
+  p = fmaf(p, z, -1.6666654611e-1f);
+  const float s = fmaf(p * z, r, r);
+  float q = fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f);
+  q = fmaf(q, z, 4.166664568298827e-2f);
+  const float c = fmaf(q * z, z, fmaf(-0.5f, z, 1.0f));
+  const int n = ((int)k) & 3;
+  sf = (n == 0) ? s : (n == 1) ? c : (n == 2) ? -s : -c;
+  cf = (n == 0) ? c : (n == 1) ? -s : (n == 2) ? -c : s;
+}
+
 // ------------------------------------------------------------ f64 helpers
-// A double constant materialised into an SGPR pair at its point of use.  The
-// megakernel loop is long and register-bound: left alone, the compiler hoists
-// the 21 sin/cos coefficients out of it into VGPR pairs, runs out of VGPRs and
-// spills them to scratch, reloading each (with a full vmcnt wait) inside the
-// polynomial.  As SGPR operands they cost two s_mov per use on the scalar pipe.
-__device__ __forceinline__ double kc(double c) {
-  asm volatile("" : "+s"(c));
-  return c;
-}
-
-// The polynomial's coefficients, read by scalar loads at their point of use
-// (IPT_TRIG_TABLE, default): kc()'s SGPR-pair constants are rematerialised
-// per use but the allocator still keeps some of them live across the loop and
-// shuffles them through VGPR lanes (v_readlane / v_writelane, VALU work).
-#ifndef IPT_TRIG_TABLE
-#define IPT_TRIG_TABLE 1
-#endif
-__constant__ double kSinCosTab[21] = {
-    0.6366197723675814,     1.5707963267948966,     6.123233995736766e-17,  // 2/pi, pi/2 hi, lo
-    2.8114572543455206e-15, -7.647163731819816e-13, 1.6059043836821613e-10, -2.505210838544172e-08,
-    2.7557319223985893e-06, -0.0001984126984126984, 0.008333333333333333,   -0.16666666666666666,
-    -1.5619206968586225e-16, 4.779477332387385e-14, -1.1470745597729725e-11, 2.08767569878681e-09,
-    -2.755731922398589e-07, 2.48015873015873e-05,   -0.001388888888888889,  0.041666666666666664,
-    -0.5,                   0.0};
-
-__device__ __forceinline__ void sincos_f(float xf, float &sf, float &cf) {
-#if IPT_TRIG_TABLE
-  int o = 0;
-  asm volatile("" : "+s"(o));  // an opaque offset: the loads stay here, not hoisted out of the loop
-  const double *T = kSinCosTab + o;
-#define IPT_KC(i, v) T[i]
-#else
-#define IPT_KC(i, v) kc(v)
-#endif
-  const double x = (double)xf;
-  const double k = rint(x * IPT_KC(0, 0.6366197723675814));
-  double r = fma(-k, IPT_KC(1, 1.5707963267948966), x);
-  r = fma(-k, IPT_KC(2, 6.123233995736766e-17), r);
-  const double z = r * r;
-  double ps = IPT_KC(3, 2.8114572543455206e-15);
-  ps = fma(ps, z, IPT_KC(4, -7.647163731819816e-13));
-  ps = fma(ps, z, IPT_KC(5, 1.6059043836821613e-10));
-  ps = fma(ps, z, IPT_KC(6, -2.505210838544172e-08));
-  ps = fma(ps, z, IPT_KC(7, 2.7557319223985893e-06));
-  ps = fma(ps, z, IPT_KC(8, -0.0001984126984126984));
-  ps = fma(ps, z, IPT_KC(9, 0.008333333333333333));
-  ps = fma(ps, z, IPT_KC(10, -0.16666666666666666));
-  const double s = fma(ps * z, r, r);
-  double pc = IPT_KC(11, -1.5619206968586225e-16);
-  pc = fma(pc, z, IPT_KC(12, 4.779477332387385e-14));
-  pc = fma(pc, z, IPT_KC(13, -1.1470745597729725e-11));
-  pc = fma(pc, z, IPT_KC(14, 2.08767569878681e-09));
-  pc = fma(pc, z, IPT_KC(15, -2.755731922398589e-07));
-  pc = fma(pc, z, IPT_KC(16, 2.48015873015873e-05));
-  pc = fma(pc, z, IPT_KC(17, -0.001388888888888889));
-  pc = fma(pc, z, IPT_KC(18, 0.041666666666666664));
-  pc = fma(pc, z, IPT_KC(19, -0.5));
-#undef IPT_KC
-  const double c = fma(pc, z, 1.0);
-  const int q = ((int)k) & 3;
-  const double so = (q == 0) ? s : (q == 1) ? c : (q == 2) ? -s : -c;
-  const double co = (q == 0) ? c : (q == 1) ? -s : (q == 2) ? -c : s;
-  sf = (float)so;
-  cf = (float)co;
-}
-
 __device__ inline double log_d(double x) {
   if (!(x > 0.0)) return x == 0.0 ? -__builtin_inf() : __builtin_nan("");
   if (x == __builtin_inf()) return x;
