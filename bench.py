@@ -72,7 +72,7 @@ SPHERE = CORNELL + [ObjectSpec(os.path.join(ASSETS, "shapes", "sphere.obj"), "*K
 # casts/sample counted by the CPU oracle over the full C2
 # frame (tools/count_casts.py -> profiles/casts_per_sample.json; re-derived
 # by tests/test_gpu_full.py::test_c2_forward_full_frame_bit_exact)
-CASTS_PER_SAMPLE = 5.694448232650757
+CASTS_PER_SAMPLE = 5.694429993629456
 N_TRIANGLES = 18
 FLOP_PER_TEST = 38          # F1 test with hoisted edge planes
 PEAK_FP32_TFLOPS = 157.3    # MI355X FP32 vector (= FP32 MFMA) peak, MI355X_MICROARCH.md
@@ -82,11 +82,11 @@ PMC_FILE = os.path.join(ROOT, "profiles", "pmc_fwd_trace_kernel.json")
 # tests actually executed, counted by the IPT_BVH_STATS build
 # (tools/bvh_stats.py -> profiles/bvh_stats.json: 38 per triangle test + 12
 # per slab test)
-CASTS_PER_SAMPLE_C3 = 5.612594664096832
-CASTS_PER_SAMPLE_PHONG = 5.586300492286682  # C3 with the Phong cube (tools/count_casts.py C3_phong_512x512x64_b4)
+CASTS_PER_SAMPLE_C3 = 5.61258190870285
+CASTS_PER_SAMPLE_PHONG = 5.586285471916199  # C3 with the Phong cube (tools/count_casts.py C3_phong_512x512x64_b4)
 # createGraph's integrator at the reference's configuration (scenes/0.txt,
 # 500x500, 100 spp, no bounce cap): tools/count_casts.py with the oracle
-CASTS_PER_SAMPLE_GRAPH = 7.12207488
+CASTS_PER_SAMPLE_GRAPH = 7.1221032
 GRAPH_TARGET = os.path.join(ROOT, "tests", "golden", "preds_0_true.png")  # the reference's preds/0_true.png
 BVH_STATS_FILE = os.path.join(ROOT, "profiles", "bvh_stats.json")
 

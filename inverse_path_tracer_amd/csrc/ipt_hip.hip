@@ -1307,8 +1307,10 @@ __global__ IPT_TRACE_BOUNDS void trace_kernel(
           float cth, sth, psamp;
           if (!spec) {
             cth = sqrt_core(ut);  // == (float)sqrt((double)ut) (innocuous double rounding); ut >= 2^-33
-            const double omu = 1.0 - (double)ut;  // 0 or >= 2^-33
-            sth = omu > 0.0 ? (float)dsqrt_core(omu) : 0.f;
+            // sin(theta) = sqrt(1 - u) from the float 1 - u (rounds 1-6: from the
+            // exact double 1 - u, 0.6% slower)
+            const float omu = 1.0f - ut;  // 0 or >= 2^-24
+            sth = omu > 0.f ? sqrt_core(omu) : 0.f;
             psamp = kInvPiF;
           } else {
             const double cd = pow_d((double)ut, 1.0 / ((double)m.shininess + 1.0));

@@ -15,7 +15,8 @@
  *    cross = fmaf(a1,b2,-(a2*b1)) ..., mat·vec rows as dot chains,
  *    normalize = three IEEE divisions by sqrtf(dot3(v,v));
  *  - the reference's double-precision pow(r,0.5) is sqrt (correctly rounded);
- *    acos/sin/cos of the hemisphere angle use sin(acos(sqrt u)) = sqrt(1-u);
+ *    acos/sin/cos of the hemisphere angle use sin(acos(sqrt u)) = sqrtf(1-u)
+ *    (1 - u in float) and cos(acos(sqrt u)) = sqrt u;
  *    sin/cos(phi) are float sinf/cosf (as the reference's float phi calls them)
  *    by one fixed fp32 reduction + polynomial, shared with the kernel.
  */
@@ -1319,7 +1320,7 @@ static v3 sample_dir(const otri_t *tri, int spec, float shin, float *psamp, xorw
   float ct, snt;
   if (!spec) {
     ct = (float)sqrt((double)ut);
-    snt = (float)sqrt(1.0 - (double)ut);
+    snt = sqrtf(1.0f - ut); /* sin(acos(sqrt u)) = sqrt(1 - u), from the float 1 - u */
     *psamp = INV_PI_F;
   } else {
     double e = 1.0 / ((double)shin + 1.0);
