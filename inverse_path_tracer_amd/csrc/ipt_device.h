@@ -115,9 +115,14 @@ __device__ __forceinline__ void sincos_f(float x, float &sf, float &cf) {
   float q = fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f);
   q = fmaf(q, z, 4.166664568298827e-2f);
   const float c = fmaf(q * z, z, fmaf(-0.5f, z, 1.0f));
-  const int n = ((int)k) & 3;
-  sf = (n == 0) ? s : (n == 1) ? c : (n == 2) ? -s : -c;
-  cf = (n == 0) ? c : (n == 1) ? -s : (n == 2) ? -c : s;
+  const int n = (int)k;
+  // the quadrant by one swap and two sign flips (bitwise the selects of
+  // s, c, -s, -c; 4 B less scratch in the 6-wave adjoint, 8 B in the
+  // unbounded one, -0.5% on both, variants_sincos_xor_r06zf.log)
+  const bool sw = (n & 1) != 0;
+  const float a = sw ? c : s, b = sw ? s : c;
+  sf = __uint_as_float(__float_as_uint(a) ^ ((uint32_t)(n & 2) << 30));
+  cf = __uint_as_float(__float_as_uint(b) ^ ((uint32_t)((n + 1) & 2) << 30));
 }
 
 // ------------------------------------------------------------ f64 helpers

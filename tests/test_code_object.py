@@ -28,16 +28,15 @@ BUDGET = {
     (0, False, False): 0,   # forward (sample buffer)
     (4, False, False): 0,   # fused render: the C2 headline
     (1, False, False): 0,   # adjoint: the C2 headline's gradient
-    (5, False, False): 12,  # adjoint at 6 waves/SIMD (80 VGPRs, full-size launches): work item + Le in LDS; one
-                            # 8-B pair reloaded once per shaded vertex since the fp32 sin/cos (round 6: 8 B, entry
-                            # only; round 5: 16 B per pair block) -- 1.736 -> 1.687 ms regardless
+    (5, False, False): 8,   # adjoint at 6 waves/SIMD (80 VGPRs, full-size launches): work item + Le in LDS
+                            # (round 5: 16 B reloaded per pair block; 12 B for one build of the fp32 sin/cos, §12.11)
     (2, False, False): 0,   # createGraph
     (2, False, True): 0,
     (1, False, True): 0,    # BVH adjoint (2 waves/SIMD, 256 VGPRs allowed)
     (3, False, True): 0,
-    (3, False, False): 20,  # unbounded adjoint: pool chunks (round 5: 8 B; round 6: 12 B with the uniform-region
+    (3, False, False): 12,  # unbounded adjoint: pool chunks (round 5: 8 B; round 6: 12 B with the uniform-region
                             # flag, DESIGN.md §12.9, under which this launch is 1.2-1.4% faster; 20 B with the fp32
-                            # sin/cos, under which it is 1.5-1.8% faster again, §12.11)
+                            # sin/cos before its quadrant select became sign flips, §12.11)
     (0, False, True): 0,    # BVH forward: the work item, source triangle and Le in LDS (round 5; was 44-52 B)
     # SPEC instances (materials with a Phong lobe): pow_d out of line keeps its
     # constants out of the trace loop (round 4: 164-292 B per lane)
